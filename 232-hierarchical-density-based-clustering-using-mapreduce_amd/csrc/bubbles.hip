@@ -1,0 +1,219 @@
+// bubbles.hip -- K4 data-bubble statistics and K5 bubble k-NN.
+//
+// K4 (CombineStep.java:18-64 / ClusterFeatureDataBubbles.java:192-215): members of a
+// bubble are folded in ascending point order (D5) -- the fold order fixes the FP sums, so
+// the points are stably radix-sorted by bubble id and each bubble is folded sequentially
+// by one lane (parallel over bubbles), then the per-bubble epilogue computes rep, extent
+// and nnDist from the final (LS, SS, n) exactly as the last CombineStep call does.
+//
+// K5 (HdbscanDataBubbles.calculateCoreDistancesBubbles, :75-146): per bubble p the lane
+// scans q != p in index order with the reference's insertion (strict '<') on the
+// transformed distance distanceBubbles(...) and logs, per buffer position, the LAST
+// neighbour inserted there during p's scan.  The reference's indexBubbles[] is never
+// reset across points (:79-83,118), so its state before point p's formula is the
+// last-writer prefix of these logs -- resolved by the host epilogue in point order.
+#include <hipcub/hipcub.hpp>
+
+#include "common.hpp"
+
+namespace hdb {
+
+__global__ void iota32_kernel(int32_t *a, int64_t n) { HDB_GRID_STRIDE(i, n) a[i] = (int32_t)i; }
+
+__global__ void bubble_count_kernel(const int32_t *__restrict__ bo, int64_t n, int64_t nb, int32_t *__restrict__ cnt,
+                                    int *__restrict__ bad) {
+    HDB_GRID_STRIDE(i, n) {
+        int32_t b = bo[i];
+        if (b < 0 || b >= nb) {
+            *bad = 1;
+            continue;
+        }
+        atomicAdd(&cnt[b], 1);
+    }
+}
+
+// one lane per bubble: sequential fold in member order
+__global__ void bubble_fold_kernel(const double *__restrict__ X, int d, const int32_t *__restrict__ perm,
+                                   const int64_t *__restrict__ off, int64_t nb, int variant,
+                                   double *__restrict__ ls, double *__restrict__ ss, double *__restrict__ rep,
+                                   double *__restrict__ info) {
+    HDB_GRID_STRIDE(b, nb) {
+        const int64_t lo = off[b], hi = off[b + 1];
+        double *L = ls + b * d, *Q = ss + b * d, *R = rep + b * d, *I = info + b * 3;
+        if (lo == hi) {
+            for (int c = 0; c < d; c++) L[c] = Q[c] = R[c] = 0;
+            I[0] = I[1] = I[2] = 0;
+            continue;
+        }
+        const double *x0 = X + (int64_t)perm[lo] * d;
+        for (int c = 0; c < d; c++) {
+            double v = x0[c];
+            L[c] = v;
+            Q[c] = v * v;
+        }
+        for (int64_t k = lo + 1; k < hi; k++) {
+            const double *x = X + (int64_t)perm[k] * d;
+            for (int c = 0; c < d; c++) {
+                double v = x[c];
+                L[c] = L[c] + v;
+                Q[c] = Q[c] + (v * v);
+            }
+        }
+        const int64_t cnt = hi - lo;
+        if (cnt == 1) {
+            for (int c = 0; c < d; c++) R[c] = L[c];  // rep = ls (FirstStep.java:100)
+            I[0] = 0;
+            I[1] = 0;
+            I[2] = 1;
+            continue;
+        }
+        if (variant == HDB_BUBBLE_COMBINESTEP) {
+            const double n = (double)cnt;  // n += 1 per call == member count (sequential fold)
+            for (int c = 0; c < d; c++) R[c] = L[c] / n;  // computeRepBubble (:58-64)
+            double extent = 0.0;                          // computeExtentBubble (:46-56)
+            for (int c = 0; c < d; c++) {
+                double v = ((2 * n * Q[c]) - (2 * (L[c] * L[c])));
+                if (v >= 0) extent += sqrt(v / (n * (n - 1)));
+            }
+            extent = extent / d;
+            I[0] = extent;
+            // computeNNDistBubble (:42-44): pow(1/n, (int)(1/d)) * extent
+            I[1] = pow((1 / n), (double)(1 / d)) * extent;
+            I[2] = n;
+        } else {
+            const int32_t n = (int32_t)cnt;
+            for (int c = 0; c < d; c++) R[c] = L[c] / n;
+            const int32_t prod = (int32_t)((uint32_t)n * (uint32_t)(n - 1));  // Java int overflow
+            double sum = 0.0;
+            for (int c = 0; c < d; c++) sum = sum + (((2 * n * Q[c]) - (2 * (L[c] * L[c]))) / prod);
+            const double extent = sqrt(sum);
+            I[0] = extent;
+            I[1] = pow((double)1 / n, (double)1 / d) * extent;
+            I[2] = n;
+        }
+    }
+}
+
+void bubble_stats_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const int32_t *bo, int64_t nb, int variant,
+                         double *ls, double *ss, double *rep, double *info) {
+    if (nb <= 0) return;
+    if (n > INT32_MAX) HDB_THROW(HDB_EINVAL, "n exceeds int32");
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+        size_t o = off;
+        off += (bytes + 255) & ~size_t(255);
+        return o;
+    };
+    size_t o_keys = carve(sizeof(int32_t) * (n + 1)), o_perm = carve(sizeof(int32_t) * (n + 1)),
+           o_iota = carve(sizeof(int32_t) * (n + 1)), o_cnt = carve(sizeof(int32_t) * (nb + 1)),
+           o_off = carve(sizeof(int64_t) * (nb + 1)), o_bad = carve(sizeof(int));
+    char *base = (char *)arena(ctx, A_WORK0, off);
+    int32_t *keys = (int32_t *)(base + o_keys), *perm = (int32_t *)(base + o_perm), *iota = (int32_t *)(base + o_iota);
+    int32_t *cnt = (int32_t *)(base + o_cnt);
+    int64_t *offs = (int64_t *)(base + o_off);
+    int *bad = (int *)(base + o_bad);
+    int g = 2048;
+    HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (nb + 1), ctx->stream));
+    HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(int), ctx->stream));
+    KernelTimer t(ctx, "bubble_stats");
+    if (n > 0) {
+        hipLaunchKernelGGL(iota32_kernel, dim3(g), dim3(256), 0, ctx->stream, iota, n);
+        hipLaunchKernelGGL(bubble_count_kernel, dim3(g), dim3(256), 0, ctx->stream, bo, n, nb, cnt, bad);
+        size_t tb = 0;
+        int end_bit = 1;
+        while (end_bit < 32 && (int64_t(1) << end_bit) < nb) end_bit++;
+        HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bo, keys, iota, perm, (int)n, 0, end_bit, ctx->stream));
+        void *tmp = arena(ctx, A_SORT, tb);
+        HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, bo, keys, iota, perm, (int)n, 0, end_bit, ctx->stream));
+    }
+    // exclusive scan of counts (int32) into int64 offsets
+    {
+        size_t tb = 0;
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, offs, (int)(nb + 1), ctx->stream));
+        void *tmp = arena(ctx, A_SORT, tb);
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, offs, (int)(nb + 1), ctx->stream));
+    }
+    hipLaunchKernelGGL(bubble_fold_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(nb, 64), 4096)), dim3(64), 0,
+                       ctx->stream, X, d, perm, offs, nb, variant, ls, ss, rep, info);
+    HIP_CHECK(hipGetLastError());
+    int h_bad = 0;
+    HIP_CHECK(hipMemcpyAsync(&h_bad, bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (h_bad) HDB_THROW(HDB_EINVAL, "bubble_of out of range");
+}
+
+// ------------------------------------------------------------ K5 bubble kNN
+// knn[b][K] final buffer (transformed distances, MAX padded); log[b][K] last neighbour
+// inserted at each position during b's scan (-1 if none).  Buffer init Double.MAX_VALUE,
+// strict '<' insertion with shift, exactly HdbscanDataBubbles.java:92-119.
+template <int KC>
+__global__ __launch_bounds__(256) void bubble_knn_kernel(const double *__restrict__ rep, const double *__restrict__ eB,
+                                                         const double *__restrict__ nnB, int64_t b, int d, int metric,
+                                                         int K, double *__restrict__ knn_out,
+                                                         int32_t *__restrict__ log_out) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t pr = p < b ? p : 0;
+    double buf[KC];
+    int32_t lg[KC];
+#pragma unroll
+    for (int k = 0; k < KC; k++) {
+        buf[k] = JMAX;
+        lg[k] = -1;
+    }
+    const double ep = eB[pr], np_ = nnB[pr];
+    const double *xp = rep + pr * d;
+    for (int64_t q = 0; q < b; q++) {  // wave-uniform loop
+        if (q == p) continue;
+        double dist = metric_distance(xp, rep + q * d, d, metric);
+        dist = distance_bubbles(dist, ep, eB[q], np_, nnB[q]);
+        // insertion: position = count of buffer entries <= dist (among the first K)
+        if (dist < buf[K - 1 < KC ? K - 1 : KC - 1]) {
+            int pos = K;
+#pragma unroll
+            for (int k = KC - 1; k >= 0; k--)
+                if (k < K && dist < buf[k]) pos = k;
+            // shift right from pos, insert
+#pragma unroll
+            for (int k = KC - 1; k > 0; k--)
+                if (k < K && k > pos) buf[k] = buf[k - 1];
+#pragma unroll
+            for (int k = 0; k < KC; k++)
+                if (k == pos) {
+                    buf[k] = dist;
+                    lg[k] = (int32_t)q;
+                }
+        }
+    }
+    if (p < b) {
+#pragma unroll
+        for (int k = 0; k < KC; k++)
+            if (k < K) {
+                knn_out[p * K + k] = buf[k];
+                log_out[p * K + k] = lg[k];
+            }
+    }
+}
+
+void bubble_knn_device(hdb_ctx *ctx, const double *rep, const double *eB, const double *nnB, int64_t b, int d,
+                       int metric, int K, double *knn_out, int32_t *log_out) {
+    if (b <= 0 || K <= 0) return;
+    dim3 grid((unsigned)ceil_div(b, 256));
+    KernelTimer t(ctx, "bubble_knn");
+    if (K <= 3)
+        hipLaunchKernelGGL(bubble_knn_kernel<3>, grid, dim3(256), 0, ctx->stream, rep, eB, nnB, b, d, metric, K, knn_out,
+                           log_out);
+    else if (K <= 7)
+        hipLaunchKernelGGL(bubble_knn_kernel<7>, grid, dim3(256), 0, ctx->stream, rep, eB, nnB, b, d, metric, K, knn_out,
+                           log_out);
+    else if (K <= 15)
+        hipLaunchKernelGGL(bubble_knn_kernel<15>, grid, dim3(256), 0, ctx->stream, rep, eB, nnB, b, d, metric, K,
+                           knn_out, log_out);
+    else if (K <= 31)
+        hipLaunchKernelGGL(bubble_knn_kernel<31>, grid, dim3(256), 0, ctx->stream, rep, eB, nnB, b, d, metric, K,
+                           knn_out, log_out);
+    else
+        HDB_THROW(HDB_EINVAL, "minPts too large (max 32)");
+    HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace hdb

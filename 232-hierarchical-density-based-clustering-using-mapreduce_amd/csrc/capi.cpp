@@ -1,0 +1,396 @@
+// capi.cpp -- extern "C" entry points of libhdbmi (declared in include/hdbmi.h).
+// Each entry: validate, select the device, stage host arrays (Stager), run the device
+// building blocks on the context stream, copy host outputs back.
+#include <algorithm>
+#include <vector>
+
+#include "internal.hpp"
+
+using namespace hdb;
+
+namespace {
+
+template <class F>
+int guarded(hdb_ctx *ctx, F &&f) {
+    try {
+        if (!ctx) HDB_THROW(HDB_EINVAL, "ctx is NULL");
+        HIP_CHECK(hipSetDevice(ctx->device));
+        f();
+        return HDB_OK;
+    } catch (const Error &e) {
+        set_error(e.msg);
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        set_error("host allocation failed");
+        return HDB_ENOMEM;
+    }
+}
+
+template <class T>
+std::vector<T> to_host(hdb_ctx *ctx, const T *p, size_t count) {
+    std::vector<T> v(count);
+    if (!count) return v;
+    if (is_device_ptr(p)) {
+        HIP_CHECK(hipMemcpyAsync(v.data(), p, sizeof(T) * count, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    } else {
+        std::copy(p, p + count, v.begin());
+    }
+    return v;
+}
+
+void check_metric(int metric) {
+    if (metric < HDB_METRIC_EUCLIDEAN || metric > HDB_METRIC_SUPREMUM) HDB_THROW(HDB_EINVAL, "unknown metric");
+}
+
+__global__ void iota_ids_kernel(int32_t *a, int64_t n) { HDB_GRID_STRIDE(i, n) a[i] = (int32_t)i; }
+
+const int32_t *identity_ids(hdb_ctx *ctx, int64_t n) {
+    int32_t *ids = (int32_t *)arena(ctx, A_STAGE_OUT, sizeof(int32_t) * std::max<int64_t>(n, 1));
+    hipLaunchKernelGGL(iota_ids_kernel, dim3(1024), dim3(256), 0, ctx->stream, ids, n);
+    HIP_CHECK(hipGetLastError());
+    return ids;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hdb_distance_rows(hdb_ctx *ctx, const double *a, const double *b, int64_t n, int32_t d, int32_t metric,
+                      double *out) {
+    return guarded(ctx, [&] {
+        check_metric(metric);
+        if (n < 0 || d <= 0 || !a || !b || !out) HDB_THROW(HDB_EINVAL, "bad arguments");
+        Stager s(ctx);
+        const double *da = s.in(a, n * d), *db = s.in(b, n * d);
+        double *dout = s.out(out, n);
+        distance_rows_device(ctx, da, db, n, d, metric, dout);
+        s.finish();
+    });
+}
+
+int hdb_core_distances(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t min_pts, int32_t metric,
+                       int32_t semantics, double *core_out) {
+    return guarded(ctx, [&] {
+        check_metric(metric);
+        if (n < 0 || d <= 0 || !X || !core_out || min_pts < 1) HDB_THROW(HDB_EINVAL, "bad arguments");
+        if (semantics < 0 || semantics > 2) HDB_THROW(HDB_EINVAL, "unknown core semantics");
+        Stager s(ctx);
+        const double *dX = s.in(X, n * d);
+        double *dc = s.out(core_out, n);
+        core_distances_device(ctx, dX, n, d, min_pts, metric, semantics, dc);
+        s.finish();
+    });
+}
+
+int hdb_knn(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t k, int32_t metric, int32_t excl_self,
+            double *dist_out, int32_t *idx_out) {
+    return guarded(ctx, [&] {
+        check_metric(metric);
+        if (n < 0 || d <= 0 || k < 1 || !X || !dist_out) HDB_THROW(HDB_EINVAL, "bad arguments");
+        Stager s(ctx);
+        const double *dX = s.in(X, n * d);
+        double *dv = s.out(dist_out, n * k);
+        int32_t *di = s.out(idx_out, n * k);
+        int KC = 0;
+        // lists with the bucket width, then compact to k columns
+        int kc_guess = k <= 1 ? 1 : (k <= 3 ? 3 : (k <= 7 ? 7 : (k <= 15 ? 15 : 31)));
+        double *lv = (double *)arena(ctx, A_WORK0, sizeof(double) * std::max<int64_t>(n * kc_guess, 1));
+        int32_t *li = di ? (int32_t *)arena(ctx, A_WORK1, sizeof(int32_t) * std::max<int64_t>(n * kc_guess, 1)) : nullptr;
+        knn_lists_device(ctx, dX, n, d, k, metric, excl_self != 0, lv, li, &KC);
+        if (n > 0) {
+            HIP_CHECK(hipMemcpy2DAsync(dv, sizeof(double) * k, lv, sizeof(double) * KC, sizeof(double) * k, n,
+                                       hipMemcpyDeviceToDevice, ctx->stream));
+            if (di)
+                HIP_CHECK(hipMemcpy2DAsync(di, sizeof(int32_t) * k, li, sizeof(int32_t) * KC, sizeof(int32_t) * k, n,
+                                           hipMemcpyDeviceToDevice, ctx->stream));
+        }
+        s.finish();
+    });
+}
+
+static void prim_common(hdb_ctx *ctx, const double *X, const int64_t *offsets, int32_t P, int32_t d,
+                        const double *core, const int32_t *ids, const double *eB, const double *nnB, int32_t metric,
+                        int32_t self_edges, int32_t *va, int32_t *vb, double *w) {
+    check_metric(metric);
+    if (P < 0 || d <= 0 || !X || !core || !va || !vb || !w) HDB_THROW(HDB_EINVAL, "bad arguments");
+    std::vector<int64_t> offs = to_host(ctx, offsets, (size_t)P + 1);
+    if (offs[0] != 0) HDB_THROW(HDB_EINVAL, "offsets[0] must be 0");
+    int64_t n = offs[P];
+    int64_t ne = 0;
+    for (int p = 0; p < P; p++) {
+        int64_t np_ = offs[p + 1] - offs[p];
+        if (np_ < 0) HDB_THROW(HDB_EINVAL, "offsets must be non-decreasing");
+        if (np_ > INT32_MAX) HDB_THROW(HDB_EINVAL, "partition too large");
+        if (np_ > 0) ne += (np_ - 1) + (self_edges ? np_ : 0);
+    }
+    Stager s(ctx);
+    PrimIn in;
+    in.X = s.in(X, n * d);
+    in.core = s.in(core, n);
+    in.ids = ids ? s.in(ids, n) : nullptr;
+    in.eB = eB ? s.in(eB, n) : nullptr;
+    in.nnB = nnB ? s.in(nnB, n) : nullptr;
+    in.d = d;
+    in.metric = metric;
+    int32_t *dva = s.out(va, ne), *dvb = s.out(vb, ne);
+    double *dw = s.out(w, ne);
+    if (!in.ids) {
+        // identity per partition: local index within each partition
+        std::vector<int32_t> h(n);
+        for (int p = 0; p < P; p++)
+            for (int64_t i = offs[p]; i < offs[p + 1]; i++) h[i] = (int32_t)(i - offs[p]);
+        int32_t *dids = (int32_t *)arena(ctx, A_STAGE_OUT, sizeof(int32_t) * std::max<int64_t>(n, 1));
+        HIP_CHECK(hipMemcpyAsync(dids, h.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        in.ids = dids;
+    }
+    prim_batched_device(ctx, in, offs.data(), P, self_edges, dva, dvb, dw);
+    s.finish();
+}
+
+int hdb_prim_mst(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const double *core, const int32_t *ids,
+                 int32_t metric, int32_t self_edges, int32_t *va, int32_t *vb, double *w) {
+    return guarded(ctx, [&] {
+        if (n < 1) HDB_THROW(HDB_EINVAL, "n must be >= 1 (new int[n-1])");
+        int64_t offs[2] = {0, n};
+        prim_common(ctx, X, offs, 1, d, core, ids, nullptr, nullptr, metric, self_edges, va, vb, w);
+    });
+}
+
+int hdb_prim_mst_batched(hdb_ctx *ctx, const double *X, const int64_t *offsets, int32_t P, int32_t d,
+                         const double *core, const int32_t *ids, int32_t metric, int32_t self_edges, int32_t *va,
+                         int32_t *vb, double *w) {
+    return guarded(ctx, [&] {
+        if (!offsets) HDB_THROW(HDB_EINVAL, "offsets is NULL");
+        prim_common(ctx, X, offsets, P, d, core, ids, nullptr, nullptr, metric, self_edges, va, vb, w);
+    });
+}
+
+int hdb_leaf_msts(hdb_ctx *ctx, const double *X, const int64_t *offsets, int32_t P, int32_t d, const int32_t *ids,
+                  int32_t min_pts, int32_t metric, double *core_out, int32_t *va, int32_t *vb, double *w) {
+    return guarded(ctx, [&] {
+        check_metric(metric);
+        if (!X || !offsets || !ids || !va || !vb || !w || P < 0 || d <= 0 || min_pts < 1)
+            HDB_THROW(HDB_EINVAL, "bad arguments");
+        std::vector<int64_t> offs = to_host(ctx, offsets, (size_t)P + 1);
+        if (offs[0] != 0) HDB_THROW(HDB_EINVAL, "offsets[0] must be 0");
+        const int64_t n = offs[P];
+        int64_t ne = 0;
+        std::vector<int32_t> small;
+        std::vector<int32_t> large;
+        for (int p = 0; p < P; p++) {
+            int64_t np_ = offs[p + 1] - offs[p];
+            if (np_ < 0) HDB_THROW(HDB_EINVAL, "offsets must be non-decreasing");
+            if (np_ > 0) ne += 2 * np_ - 1;
+            if (np_ > 0 && np_ <= 4096) small.push_back(p);
+            else if (np_ > 4096) large.push_back(p);
+        }
+        Stager s(ctx);
+        const double *dX = s.in(X, n * d);
+        const int32_t *dids = s.in(ids, n);
+        int32_t *dva = s.out(va, ne), *dvb = s.out(vb, ne);
+        double *dw = s.out(w, ne);
+        double *dcore = core_out ? s.out(core_out, n)
+                                 : (double *)arena(ctx, A_STAGE_OUT, sizeof(double) * std::max<int64_t>(n, 1));
+        if (min_pts == 1) {
+            HIP_CHECK(hipMemsetAsync(dcore, 0, sizeof(double) * std::max<int64_t>(n, 0), ctx->stream));
+        } else {
+            // offsets + small list on device
+            int64_t *d_off = (int64_t *)arena(ctx, A_STAGE_IN, sizeof(int64_t) * (P + 1) + sizeof(int32_t) * (P + 1) + 256);
+            int32_t *d_parts = (int32_t *)((char *)d_off + ((sizeof(int64_t) * (P + 1) + 255) & ~size_t(255)));
+            HIP_CHECK(hipMemcpyAsync(d_off, offs.data(), sizeof(int64_t) * (P + 1), hipMemcpyHostToDevice, ctx->stream));
+            if (!small.empty())
+                HIP_CHECK(hipMemcpyAsync(d_parts, small.data(), sizeof(int32_t) * small.size(), hipMemcpyHostToDevice,
+                                         ctx->stream));
+            leaf_cores_device(ctx, dX, d, metric, P, d_off, d_parts, (int)small.size(), n, min_pts - 1, dcore);
+            HIP_CHECK(hipStreamSynchronize(ctx->stream));  // d_off/d_parts live in a reused arena
+            for (int32_t p : large)
+                core_distances_device(ctx, dX + offs[p] * d, offs[p + 1] - offs[p], d, min_pts, metric,
+                                      HDB_CORE_INCL_SELF_CUMULATIVE, dcore + offs[p]);
+        }
+        PrimIn in;
+        in.X = dX;
+        in.core = dcore;
+        in.ids = dids;
+        in.eB = in.nnB = nullptr;
+        in.d = d;
+        in.metric = metric;
+        prim_batched_device(ctx, in, offs.data(), P, 1, dva, dvb, dw);
+        s.finish();
+    });
+}
+
+int hdb_mst_boruvka(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const double *core, int32_t metric,
+                    int32_t self_edges, int32_t *va, int32_t *vb, double *w) {
+    return guarded(ctx, [&] {
+        check_metric(metric);
+        if (n < 1 || d <= 0 || !X || !core || !va || !vb || !w) HDB_THROW(HDB_EINVAL, "bad arguments");
+        int64_t ne = (n - 1) + (self_edges ? n : 0);
+        Stager s(ctx);
+        const double *dX = s.in(X, n * d);
+        const double *dc = s.in(core, n);
+        int32_t *dva = s.out(va, ne), *dvb = s.out(vb, ne);
+        double *dw = s.out(w, ne);
+        boruvka_device(ctx, dX, n, d, dc, metric, dva, dvb, dw);
+        if (self_edges) {
+            // self edges (v, v, core[v]) after the n-1 tree edges
+            std::vector<int32_t> iv(n);
+            for (int64_t i = 0; i < n; i++) iv[i] = (int32_t)i;
+            HIP_CHECK(hipMemcpyAsync(dva + (n - 1), iv.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+            HIP_CHECK(hipMemcpyAsync(dvb + (n - 1), iv.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+            HIP_CHECK(hipMemcpyAsync(dw + (n - 1), dc, sizeof(double) * n, hipMemcpyDeviceToDevice, ctx->stream));
+            HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        }
+        s.finish();
+    });
+}
+
+int hdb_nearest_sample(hdb_ctx *ctx, const double *X, int64_t n, const double *S, int64_t m, int32_t d,
+                       int32_t metric, const int32_t *x_key, const int32_t *s_key, int32_t *nearest_out,
+                       double *dist_out) {
+    return guarded(ctx, [&] {
+        check_metric(metric);
+        if (n < 0 || m < 0 || d <= 0 || !X || (!S && m > 0) || !nearest_out) HDB_THROW(HDB_EINVAL, "bad arguments");
+        if ((x_key == nullptr) != (s_key == nullptr)) HDB_THROW(HDB_EINVAL, "x_key and s_key go together");
+        Stager s(ctx);
+        const double *dX = s.in(X, n * d);
+        const double *dS = m ? s.in(S, m * d) : nullptr;
+        const int32_t *dxk = s.in(x_key, n), *dsk = s.in(s_key, m);
+        int32_t *dn = s.out(nearest_out, n);
+        double *dd = s.out(dist_out, n);
+        nearest_sample_device(ctx, dX, n, dS, m, d, metric, dxk, dsk, dn, dd);
+        s.finish();
+    });
+}
+
+int hdb_bubble_stats(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const int32_t *bubble_of, int64_t nb,
+                     int32_t variant, double *ls, double *ss, double *rep, double *info) {
+    return guarded(ctx, [&] {
+        if (n < 0 || nb < 0 || d <= 0 || (!X && n) || (!bubble_of && n) || !ls || !ss || !rep || !info)
+            HDB_THROW(HDB_EINVAL, "bad arguments");
+        if (variant != HDB_BUBBLE_COMBINESTEP && variant != HDB_BUBBLE_CF) HDB_THROW(HDB_EINVAL, "unknown variant");
+        Stager s(ctx);
+        const double *dX = s.in(X, n * d);
+        const int32_t *dbo = s.in(bubble_of, n);
+        double *dls = s.out(ls, nb * d), *dss = s.out(ss, nb * d), *drep = s.out(rep, nb * d), *dinfo = s.out(info, nb * 3);
+        bubble_stats_device(ctx, dX, n, d, dbo, nb, variant, dls, dss, drep, dinfo);
+        s.finish();
+    });
+}
+
+static void bubble_core_impl(hdb_ctx *ctx, const double *rep, const int32_t *nB, const double *eB, const double *nnB,
+                             int64_t b, int32_t d, int32_t min_pts, int32_t metric, std::vector<double> &core_h) {
+    const int K = min_pts - 1;
+    core_h.assign(b, 0.0);
+    if (min_pts == 1 || b == 0) return;
+    Stager s(ctx);
+    const double *drep = s.in(rep, b * d), *deB = s.in(eB, b), *dnnB = s.in(nnB, b);
+    double *knn = (double *)arena(ctx, A_WORK0, sizeof(double) * b * K);
+    int32_t *lg = (int32_t *)arena(ctx, A_WORK1, sizeof(int32_t) * b * K);
+    bubble_knn_device(ctx, drep, deB, dnnB, b, d, metric, K, knn, lg);
+    std::vector<double> knn_h = to_host(ctx, (const double *)knn, (size_t)(b * K));
+    std::vector<int32_t> lg_h = to_host(ctx, (const int32_t *)lg, (size_t)(b * K));
+    std::vector<double> rep_h = to_host(ctx, rep, (size_t)(b * d)), eB_h = to_host(ctx, eB, (size_t)b),
+                        nnB_h = to_host(ctx, nnB, (size_t)b);
+    std::vector<int32_t> nB_h = to_host(ctx, nB, (size_t)b);
+    int rc = bubble_core_epilogue(rep_h.data(), nB_h.data(), eB_h.data(), nnB_h.data(), b, d, min_pts, metric,
+                                  knn_h.data(), lg_h.data(), core_h.data());
+    if (rc) HDB_THROW(rc, "calculateCoreDistancesBubbles raised a reference exception");
+    s.finish();
+}
+
+int hdb_bubble_core_distances(hdb_ctx *ctx, const double *rep, const int32_t *nB, const double *eB,
+                              const double *nnB, int64_t b, int32_t d, int32_t min_pts, int32_t metric,
+                              double *core_out) {
+    return guarded(ctx, [&] {
+        check_metric(metric);
+        if (b < 0 || d <= 0 || min_pts < 1 || !rep || !nB || !eB || !nnB || !core_out)
+            HDB_THROW(HDB_EINVAL, "bad arguments");
+        if (min_pts > 32) HDB_THROW(HDB_EINVAL, "minPts too large (max 32)");
+        std::vector<double> core_h;
+        bubble_core_impl(ctx, rep, nB, eB, nnB, b, d, min_pts, metric, core_h);
+        if (is_device_ptr(core_out)) {
+            HIP_CHECK(hipMemcpyAsync(core_out, core_h.data(), sizeof(double) * b, hipMemcpyHostToDevice, ctx->stream));
+            HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        } else {
+            std::copy(core_h.begin(), core_h.end(), core_out);
+        }
+    });
+}
+
+int hdb_bubble_prim_mst(hdb_ctx *ctx, const double *rep, const double *eB, const double *nnB,
+                        const int32_t *id_bubbles, const double *core, int64_t b, int32_t d, int32_t metric,
+                        int32_t self_edges, int32_t *va, int32_t *vb, double *w) {
+    return guarded(ctx, [&] {
+        if (b < 1) HDB_THROW(HDB_EINVAL, "b must be >= 1");
+        if (!eB || !nnB) HDB_THROW(HDB_EINVAL, "eB/nnB required");
+        int64_t offs[2] = {0, b};
+        prim_common(ctx, rep, offs, 1, d, core, id_bubbles, eB, nnB, metric, self_edges, va, vb, w);
+    });
+}
+
+int hdb_quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne) {
+    if (!va || !vb || !w || ne < 0) return HDB_EINVAL;
+    int rc = quicksort_edges(va, vb, w, ne);
+    if (rc) set_error("quicksortByEdgeWeight: stack overflow (ArrayIndexOutOfBoundsException)");
+    return rc;
+}
+
+int hdb_local_model(hdb_ctx *ctx, const double *rep, const double *info, int64_t b, int32_t d, int32_t min_pts,
+                    int32_t min_cl_size, int32_t metric, int32_t *labels, int32_t *mst_va, int32_t *mst_vb,
+                    double *mst_w, int32_t *ic_va, int32_t *ic_vb, double *ic_w, int64_t *n_ic) {
+    return guarded(ctx, [&] {
+        check_metric(metric);
+        if (b < 1 || d <= 0 || !rep || !info || !labels || min_pts < 1) HDB_THROW(HDB_EINVAL, "bad arguments");
+        if (min_pts > 32) HDB_THROW(HDB_EINVAL, "minPts too large (max 32)");
+        std::vector<double> rep_h = to_host(ctx, rep, (size_t)(b * d));
+        std::vector<double> info_h = to_host(ctx, info, (size_t)(b * 3));
+        std::vector<double> eB(b), nnB(b);
+        std::vector<int32_t> nB(b), ids(b);
+        for (int64_t i = 0; i < b; i++) {  // LocalModelReduceByKey.java:80-84
+            eB[i] = info_h[i * 3 + 0];
+            nnB[i] = info_h[i * 3 + 1];
+            nB[i] = (int32_t)info_h[i * 3 + 2];
+            ids[i] = (int32_t)i;  // D4: vertex id == position
+        }
+        std::vector<double> core;
+        bubble_core_impl(ctx, rep_h.data(), nB.data(), eB.data(), nnB.data(), b, d, min_pts, metric, core);
+        const int64_t ne = 2 * b - 1;
+        std::vector<int32_t> mva(ne), mvb(ne);
+        std::vector<double> mw(ne);
+        {
+            int64_t offs[2] = {0, b};
+            prim_common(ctx, rep_h.data(), offs, 1, d, core.data(), ids.data(), eB.data(), nnB.data(), metric, 1,
+                        mva.data(), mvb.data(), mw.data());
+        }
+        std::vector<int32_t> lab(b);
+        std::vector<int32_t> iva(ne), ivb(ne);
+        std::vector<double> iw(ne);
+        int64_t nic = 0;
+        int rc = local_model_host(rep_h.data(), eB.data(), nnB.data(), nB.data(), b, d, min_cl_size, metric, mva.data(),
+                                  mvb.data(), mw.data(), lab.data(), iva.data(), ivb.data(), iw.data(), &nic);
+        if (rc) HDB_THROW(rc, "local model raised a reference exception");
+        std::copy(lab.begin(), lab.end(), labels);
+        if (mst_va) std::copy(mva.begin(), mva.end(), mst_va);
+        if (mst_vb) std::copy(mvb.begin(), mvb.end(), mst_vb);
+        if (mst_w) std::copy(mw.begin(), mw.end(), mst_w);
+        if (ic_va) std::copy(iva.begin(), iva.begin() + nic, ic_va);
+        if (ic_vb) std::copy(ivb.begin(), ivb.begin() + nic, ic_vb);
+        if (ic_w) std::copy(iw.begin(), iw.begin() + nic, ic_w);
+        if (n_ic) *n_ic = nic;
+    });
+}
+
+int hdb_sort_edges_desc(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne) {
+    return guarded(ctx, [&] {
+        if (ne < 0 || (ne > 0 && (!va || !vb || !w))) HDB_THROW(HDB_EINVAL, "bad arguments");
+        Stager s(ctx);
+        int32_t *dva = s.inout(va, ne), *dvb = s.inout(vb, ne);
+        double *dw = s.inout(w, ne);
+        sort_edges_desc_device(ctx, dva, dvb, dw, ne);
+        s.finish();
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,204 @@
+// common.hpp -- shared internals of libhdbmi (context, staging, errors, metrics).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/hdbmi.h"
+
+namespace hdb {
+
+constexpr double JMAX = DBL_MAX;  // Double.MAX_VALUE
+
+// ----------------------------------------------------------------- errors
+void set_error(const std::string &msg);
+struct Error {
+    int code;
+    std::string msg;
+};
+#define HDB_THROW(code, msg) throw ::hdb::Error{(code), (msg)}
+#define HIP_CHECK(expr)                                                                      \
+    do {                                                                                     \
+        hipError_t _e = (expr);                                                              \
+        if (_e != hipSuccess)                                                                \
+            HDB_THROW(HDB_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));       \
+    } while (0)
+
+// ---------------------------------------------------------------- context
+struct TimedLaunch {
+    std::string name;
+    hipEvent_t a, b;
+};
+
+struct Arena {  // grow-only device scratch, stream ordered reuse
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace hdb
+
+struct hdb_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    bool timing = false;
+    std::vector<hdb::TimedLaunch> pending;
+    std::vector<hipEvent_t> event_pool;
+    std::map<std::string, std::pair<double, int64_t>> acc;
+    hdb::Arena arenas[8];
+    int num_cus = 256;
+};
+
+namespace hdb {
+
+// scratch slot ids
+enum { A_STAGE_IN = 0, A_STAGE_OUT = 1, A_WORK0 = 2, A_WORK1 = 3, A_WORK2 = 4, A_WORK3 = 5, A_PAD = 6, A_SORT = 7 };
+
+void *arena(hdb_ctx *ctx, int slot, size_t bytes);
+
+// kernel timing helpers: begin/end around a launch of a named kernel
+void time_begin(hdb_ctx *ctx, const char *name, TimedLaunch &t);
+void time_end(hdb_ctx *ctx, TimedLaunch &t);
+struct KernelTimer {
+    hdb_ctx *ctx;
+    TimedLaunch t;
+    bool on;
+    KernelTimer(hdb_ctx *c, const char *name) : ctx(c), on(c->timing) {
+        if (on) time_begin(ctx, name, t);
+    }
+    ~KernelTimer() {
+        if (on) time_end(ctx, t);
+    }
+};
+
+// ---------------------------------------------------- host/device staging
+bool is_device_ptr(const void *p);
+
+// Staging of caller arrays: device pointers pass through, host pointers are copied.
+class Stager {
+   public:
+    explicit Stager(hdb_ctx *ctx) : ctx_(ctx) {}
+    ~Stager();
+    // input array (nullable)
+    template <class T>
+    const T *in(const T *p, size_t count) {
+        return static_cast<const T *>(in_raw(p, count * sizeof(T)));
+    }
+    // output array (nullable); copied back at finish()
+    template <class T>
+    T *out(T *p, size_t count) {
+        return static_cast<T *>(out_raw(p, count * sizeof(T), false));
+    }
+    // in/out array
+    template <class T>
+    T *inout(T *p, size_t count) {
+        return static_cast<T *>(out_raw(p, count * sizeof(T), true));
+    }
+    // copy host outputs back and synchronise if any host pointer was involved
+    void finish();
+    bool any_host() const { return any_host_; }
+
+   private:
+    const void *in_raw(const void *p, size_t bytes);
+    void *out_raw(void *p, size_t bytes, bool copy_in);
+    hdb_ctx *ctx_;
+    struct Buf {
+        void *dev;
+        void *host_dst;
+        size_t bytes;
+    };
+    std::vector<Buf> bufs_;
+    bool any_host_ = false;
+    bool finished_ = false;
+};
+
+// ------------------------------------------------------------- device side
+// Euclidean squared distance in the reference's exact operation order
+// (EuclideanDistance.java:31-33): s = 0 + t0 + t1 + ..., t_i = (a_i - b_i) * (a_i - b_i).
+// 0 + t0 == t0 bitwise because t0 >= +0 or NaN.  Built with -ffp-contract=off.
+__device__ __forceinline__ double sq_diff(double a, double b) {
+    double t = a - b;
+    return t * t;
+}
+
+// generic metric over runtime d (reference order for each metric)
+__device__ __forceinline__ double metric_distance(const double *a, const double *b, int d, int metric) {
+    if (metric == HDB_METRIC_EUCLIDEAN) {
+        double s = sq_diff(a[0], b[0]);
+        for (int i = 1; i < d; i++) s = s + sq_diff(a[i], b[i]);
+        return sqrt(s);
+    } else if (metric == HDB_METRIC_COSINE) {
+        double dot = 0, m1 = 0, m2 = 0;
+        for (int i = 0; i < d; i++) {
+            dot = dot + a[i] * b[i];
+            m1 = m1 + a[i] * a[i];
+            m2 = m2 + b[i] * b[i];
+        }
+        return 1 - (dot / sqrt(m1 * m2));
+    } else if (metric == HDB_METRIC_PEARSON) {
+        double mean1 = 0, mean2 = 0;
+        for (int i = 0; i < d; i++) {
+            mean1 = mean1 + a[i];
+            mean2 = mean2 + b[i];
+        }
+        mean1 = mean1 / d;
+        mean2 = mean2 / d;
+        double cov = 0, s1 = 0, s2 = 0;
+        for (int i = 0; i < d; i++) {
+            cov = cov + (a[i] - mean1) * (b[i] - mean2);
+            s1 = s1 + (a[i] - mean1) * (a[i] - mean1);
+            s2 = s2 + (b[i] - mean2) * (b[i] - mean2);
+        }
+        return 1 - (cov / sqrt(s1 * s2));
+    } else if (metric == HDB_METRIC_MANHATTAN) {
+        double s = 0;
+        for (int i = 0; i < d; i++) s = s + fabs(a[i] - b[i]);
+        return s;
+    } else {  // supremum
+        double s = 0;
+        for (int i = 0; i < d; i++) {
+            double diff = fabs(a[i] - b[i]);
+            if (diff > s) s = diff;
+        }
+        return s;
+    }
+}
+
+// HdbscanDataBubbles.distanceBubbles (HdbscanDataBubbles.java:592-600), exact order.
+__device__ __forceinline__ double distance_bubbles(double distance, double ep, double eq, double np_,
+                                                   double nq) {
+    double verify = distance - (ep + eq);
+    if (verify >= 0) return (distance - (ep + eq)) + (np_ + nq);
+    // Math.max: NaN if either argument is NaN
+    if (np_ != np_ || nq != nq) return NAN;
+    return np_ >= nq ? np_ : nq;
+}
+
+// Java Math.max(a, b) for doubles without NaN (-0.0 handling irrelevant here)
+__device__ __forceinline__ double jmax_sel(double a, double b) { return (a > b) ? a : b; }
+
+// argmin combine with the reference Prim select rule: smaller value wins, equal values ->
+// the LARGER index (HDBSCANStar.java:177-180 '<=').  idx < 0 marks "no candidate".
+__device__ __forceinline__ void argmin_last(double &v, int &i, double v2, int i2) {
+    if (i2 < 0) return;
+    if (i < 0 || v2 < v || (v2 == v && i2 > i)) {
+        v = v2;
+        i = i2;
+    }
+}
+
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// grid-stride helper
+#define HDB_GRID_STRIDE(i, n)                                                                   \
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)(n);        \
+         i += (int64_t)blockDim.x * gridDim.x)
+
+}  // namespace hdb

@@ -1,0 +1,215 @@
+// context.cpp -- hdb_ctx lifetime, scratch arenas, kernel timing, host/device staging.
+#include "common.hpp"
+
+namespace hdb {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string &msg) { g_last_error = msg; }
+const char *last_error() { return g_last_error.c_str(); }
+
+void *arena(hdb_ctx *ctx, int slot, size_t bytes) {
+    Arena &a = ctx->arenas[slot];
+    if (bytes == 0) bytes = 16;
+    if (a.bytes < bytes) {
+        if (a.ptr) {
+            // the old buffer may still be in use by queued work on this stream
+            HIP_CHECK(hipStreamSynchronize(ctx->stream));
+            HIP_CHECK(hipFree(a.ptr));
+            a.ptr = nullptr;
+        }
+        size_t nb = bytes + bytes / 4 + 4096;
+        HIP_CHECK(hipMalloc(&a.ptr, nb));
+        a.bytes = nb;
+    }
+    return a.ptr;
+}
+
+static hipEvent_t get_event(hdb_ctx *ctx) {
+    if (!ctx->event_pool.empty()) {
+        hipEvent_t e = ctx->event_pool.back();
+        ctx->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    return e;
+}
+
+void time_begin(hdb_ctx *ctx, const char *name, TimedLaunch &t) {
+    t.name = name;
+    t.a = get_event(ctx);
+    t.b = get_event(ctx);
+    HIP_CHECK(hipEventRecord(t.a, ctx->stream));
+}
+void time_end(hdb_ctx *ctx, TimedLaunch &t) {
+    HIP_CHECK(hipEventRecord(t.b, ctx->stream));
+    ctx->pending.push_back(t);
+}
+
+static void drain_timing(hdb_ctx *ctx) {
+    for (auto &t : ctx->pending) {
+        HIP_CHECK(hipEventSynchronize(t.b));
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, t.a, t.b));
+        auto &e = ctx->acc[t.name];
+        e.first += ms;
+        e.second += 1;
+        ctx->event_pool.push_back(t.a);
+        ctx->event_pool.push_back(t.b);
+    }
+    ctx->pending.clear();
+}
+
+bool is_device_ptr(const void *p) {
+    if (!p) return false;
+    hipPointerAttribute_t attr;
+    hipError_t e = hipPointerGetAttributes(&attr, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+Stager::~Stager() {
+    for (auto &b : bufs_)
+        if (b.dev) (void)hipFreeAsync(b.dev, ctx_->stream);
+}
+
+const void *Stager::in_raw(const void *p, size_t bytes) {
+    if (!p) return nullptr;
+    if (is_device_ptr(p)) return p;
+    any_host_ = true;
+    void *d = nullptr;
+    HIP_CHECK(hipMallocAsync(&d, bytes ? bytes : 16, ctx_->stream));
+    bufs_.push_back({d, nullptr, bytes});
+    if (bytes) HIP_CHECK(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx_->stream));
+    return d;
+}
+
+void *Stager::out_raw(void *p, size_t bytes, bool copy_in) {
+    if (!p) return nullptr;
+    if (is_device_ptr(p)) return p;
+    any_host_ = true;
+    void *d = nullptr;
+    HIP_CHECK(hipMallocAsync(&d, bytes ? bytes : 16, ctx_->stream));
+    bufs_.push_back({d, p, bytes});
+    if (copy_in && bytes) HIP_CHECK(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx_->stream));
+    return d;
+}
+
+void Stager::finish() {
+    if (finished_) return;
+    finished_ = true;
+    for (auto &b : bufs_)
+        if (b.host_dst && b.bytes)
+            HIP_CHECK(hipMemcpyAsync(b.host_dst, b.dev, b.bytes, hipMemcpyDeviceToHost, ctx_->stream));
+    if (any_host_) HIP_CHECK(hipStreamSynchronize(ctx_->stream));
+}
+
+}  // namespace hdb
+
+using namespace hdb;
+
+extern "C" {
+
+const char *hdb_last_error(void) { return hdb::last_error(); }
+int hdb_version(void) { return 100; }
+
+int hdb_ctx_create(int device, hdb_ctx **out) {
+    try {
+        if (!out) HDB_THROW(HDB_EINVAL, "out is NULL");
+        int count = 0;
+        HIP_CHECK(hipGetDeviceCount(&count));
+        if (device < 0 || device >= count) HDB_THROW(HDB_EDEVICE, "no such HIP device");
+        HIP_CHECK(hipSetDevice(device));
+        hdb_ctx *c = new hdb_ctx();
+        c->device = device;
+        HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->own_stream = true;
+        hipDeviceProp_t prop;
+        HIP_CHECK(hipGetDeviceProperties(&prop, device));
+        c->num_cus = prop.multiProcessorCount;
+        *out = c;
+        return HDB_OK;
+    } catch (const Error &e) {
+        set_error(e.msg);
+        return e.code;
+    }
+}
+
+void hdb_ctx_destroy(hdb_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto &t : ctx->pending) {
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+    for (auto &a : ctx->arenas)
+        if (a.ptr) (void)hipFree(a.ptr);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int hdb_ctx_set_stream(hdb_ctx *ctx, void *stream) {
+    try {
+        if (!ctx) HDB_THROW(HDB_EINVAL, "ctx is NULL");
+        HIP_CHECK(hipSetDevice(ctx->device));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        if (ctx->own_stream) HIP_CHECK(hipStreamDestroy(ctx->stream));
+        if (stream) {
+            ctx->stream = (hipStream_t)stream;
+            ctx->own_stream = false;
+        } else {
+            HIP_CHECK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+            ctx->own_stream = true;
+        }
+        return HDB_OK;
+    } catch (const Error &e) {
+        set_error(e.msg);
+        return e.code;
+    }
+}
+
+int hdb_ctx_set_timing(hdb_ctx *ctx, int enable) {
+    if (!ctx) return HDB_EINVAL;
+    ctx->timing = enable != 0;
+    return HDB_OK;
+}
+
+int hdb_ctx_kernel_time(hdb_ctx *ctx, const char *name, double *ms_total, int64_t *launches, int reset) {
+    try {
+        if (!ctx || !name) HDB_THROW(HDB_EINVAL, "NULL argument");
+        HIP_CHECK(hipSetDevice(ctx->device));
+        drain_timing(ctx);
+        auto it = ctx->acc.find(name);
+        double ms = 0;
+        int64_t n = 0;
+        if (it != ctx->acc.end()) {
+            ms = it->second.first;
+            n = it->second.second;
+            if (reset) ctx->acc.erase(it);
+        }
+        if (ms_total) *ms_total = ms;
+        if (launches) *launches = n;
+        return HDB_OK;
+    } catch (const Error &e) {
+        set_error(e.msg);
+        return e.code;
+    }
+}
+
+int hdb_ctx_synchronize(hdb_ctx *ctx) {
+    try {
+        if (!ctx) HDB_THROW(HDB_EINVAL, "ctx is NULL");
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        return HDB_OK;
+    } catch (const Error &e) {
+        set_error(e.msg);
+        return e.code;
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,45 @@
+// internal.hpp -- device-side building blocks shared by the C-ABI layer.
+#pragma once
+#include "common.hpp"
+
+namespace hdb {
+
+struct PrimIn {
+    const double *X;
+    const double *core;
+    const int32_t *ids;
+    const double *eB;
+    const double *nnB;
+    int d;
+    int metric;
+};
+
+void pack_rows(hdb_ctx *ctx, const double *X, int64_t n, int d, int dp, double *Xp);
+void knn_lists_device(hdb_ctx *ctx, const double *X_dev, int64_t n, int d, int k, int metric, bool excl,
+                      double *lists_v, int32_t *lists_i, int *KC_out);
+void core_distances_device(hdb_ctx *ctx, const double *X_dev, int64_t n, int d, int min_pts, int metric,
+                           int semantics, double *core);
+void prim_batched_device(hdb_ctx *ctx, const PrimIn &in, const int64_t *h_offs, int P, int self_edges, int32_t *va,
+                         int32_t *vb, double *w);
+void leaf_cores_device(hdb_ctx *ctx, const double *X, int d, int metric, int P, const int64_t *d_off,
+                       const int32_t *d_parts, int np, int64_t total_rows, int K, double *core);
+void nearest_sample_device(hdb_ctx *ctx, const double *X, int64_t n, const double *S, int64_t m, int d, int metric,
+                           const int32_t *xkey, const int32_t *skey, int32_t *out_i, double *out_d);
+void bubble_stats_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const int32_t *bo, int64_t nb, int variant,
+                         double *ls, double *ss, double *rep, double *info);
+void bubble_knn_device(hdb_ctx *ctx, const double *rep, const double *eB, const double *nnB, int64_t b, int d,
+                       int metric, int K, double *knn_out, int32_t *log_out);
+void sort_edges_desc_device(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne);
+void distance_rows_device(hdb_ctx *ctx, const double *a, const double *b, int64_t n, int d, int metric, double *out);
+void boruvka_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const double *core, int metric, int32_t *va,
+                    int32_t *vb, double *w);
+
+// host logic (local_model.cpp)
+int bubble_core_epilogue(const double *rep, const int32_t *nB, const double *eB, const double *nnB, int64_t b, int d,
+                         int min_pts, int metric, const double *knn, const int32_t *log, double *core);
+int quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne);
+int local_model_host(const double *rep, const double *eB, const double *nnB, const int32_t *nB, int64_t b, int d,
+                     int32_t min_cl_size, int metric, int32_t *mva, int32_t *mvb, double *mw, int32_t *labels,
+                     int32_t *ic_va, int32_t *ic_vb, double *ic_w, int64_t *n_ic);
+
+}  // namespace hdb

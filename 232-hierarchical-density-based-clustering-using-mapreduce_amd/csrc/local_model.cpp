@@ -1,0 +1,451 @@
+// local_model.cpp -- host side of LocalModelReduceByKey (LocalModelReduceByKey.java:88-104).
+//
+// The b^2 work (bubble k-NN, bubble Prim) runs in the HIP kernels; what stays here is the
+// O(b)-state logic whose result depends on Java collection semantics:
+//   * the bubble-core formula over the never-reset indexBubbles[] (HdbscanDataBubbles.java:121-143),
+//   * UndirectedGraph.quicksortByEdgeWeight (UndirectedGraph.java:93-208),
+//   * constructClusterTree (HdbscanDataBubbles.java:256-375) incl. java.util.HashMap key order,
+//   * findProminentClustersAndClassificationNoiseBubbles (:377-504),
+//   * findInterClusterEdges (:506-527).
+// Host C++ built with -ffp-contract=off so the few host distance evaluations match Java.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <numeric>
+#include <vector>
+
+#include "common.hpp"
+
+namespace hdb {
+
+// ------------------------------------------------------------- host metrics
+static double host_distance(const double *a, const double *b, int d, int metric) {
+    switch (metric) {
+    case HDB_METRIC_EUCLIDEAN: {
+        double s = 0;
+        for (int i = 0; i < d; i++) s += ((a[i] - b[i]) * (a[i] - b[i]));
+        return std::sqrt(s);
+    }
+    case HDB_METRIC_COSINE: {
+        double dot = 0, m1 = 0, m2 = 0;
+        for (int i = 0; i < d; i++) {
+            dot += (a[i] * b[i]);
+            m1 += (a[i] * a[i]);
+            m2 += (b[i] * b[i]);
+        }
+        return 1 - (dot / std::sqrt(m1 * m2));
+    }
+    case HDB_METRIC_PEARSON: {
+        double mean1 = 0, mean2 = 0;
+        for (int i = 0; i < d; i++) {
+            mean1 += a[i];
+            mean2 += b[i];
+        }
+        mean1 = mean1 / d;
+        mean2 = mean2 / d;
+        double cov = 0, s1 = 0, s2 = 0;
+        for (int i = 0; i < d; i++) {
+            cov += ((a[i] - mean1) * (b[i] - mean2));
+            s1 += ((a[i] - mean1) * (a[i] - mean1));
+            s2 += ((b[i] - mean2) * (b[i] - mean2));
+        }
+        return (1 - (cov / std::sqrt(s1 * s2)));
+    }
+    case HDB_METRIC_MANHATTAN: {
+        double s = 0;
+        for (int i = 0; i < d; i++) s += std::fabs(a[i] - b[i]);
+        return s;
+    }
+    default: {
+        double s = 0;
+        for (int i = 0; i < d; i++) {
+            double df = std::fabs(a[i] - b[i]);
+            if (df > s) s = df;
+        }
+        return s;
+    }
+    }
+}
+
+static double host_distance_bubbles(double distance, const double *eB, const double *nnB, int64_t p, int64_t q) {
+    double verify = distance - (eB[p] + eB[q]);
+    if (verify >= 0) return (distance - (eB[p] + eB[q])) + (nnB[p] + nnB[q]);
+    if (std::isnan(nnB[p]) || std::isnan(nnB[q])) return NAN;
+    return nnB[p] >= nnB[q] ? nnB[p] : nnB[q];
+}
+
+// ------------------------------------------- bubble core formula (epilogue)
+// knn/log from bubble_knn_kernel; indexBubbles state carried across points in order.
+int bubble_core_epilogue(const double *rep, const int32_t *nB, const double *eB, const double *nnB, int64_t b, int d,
+                         int min_pts, int metric, const double *knn, const int32_t *log, double *core) {
+    const int K = min_pts - 1;
+    for (int64_t i = 0; i < b; i++) core[i] = 0;
+    if (min_pts == 1) return HDB_OK;
+    std::vector<int32_t> idx(K, 0);  // indexBubbles, zero-initialised once (:79-83)
+    const int inv_d = 1 / d;
+    for (int64_t p = 0; p < b; p++) {
+        for (int k = 0; k < K; k++)
+            if (log[p * K + k] >= 0) idx[k] = log[p * K + k];
+        const double *kn = knn + p * K;
+        if (nB[p] >= K) {
+            core[p] = std::pow((double)(K / nB[p]), (double)inv_d) * eB[p];
+        } else {
+            int32_t nX = nB[p];
+            int i = 0;
+            while (nX < K) {
+                if (i >= K) return HDB_EREF_OOB;
+                nX += nB[idx[i]];
+                i += 1;
+            }
+            int32_t sum = nB[p];
+            int32_t aux = 0;
+            if (i >= b) return HDB_EREF_OOB;
+            for (int j = 0; j < i; j++) {
+                double dc = host_distance(rep + (int64_t)idx[j] * d, rep + (int64_t)i * d, d, metric);
+                dc = host_distance_bubbles(dc, eB, nnB, idx[j], i);
+                if (sum < K && kn[j] < dc) aux = K - sum;
+                sum += nB[idx[j]];
+            }
+            if (i >= K) return HDB_EREF_OOB;
+            if (nB[i] == 0) return HDB_EREF_DIVZERO;
+            core[p] = kn[i] + std::pow((double)(aux / nB[i]), (double)inv_d) * eB[i];
+        }
+    }
+    return HDB_OK;
+}
+
+// --------------------------------------------------------------- quicksort
+int quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne) {
+    if (ne <= 1) return HDB_OK;
+    const int64_t cap = ne / 2;  // new int[edgeWeights.length / 2] (:97-98)
+    std::vector<int64_t> ss(cap), es(cap);
+    auto swp = [&](int64_t i, int64_t j) {
+        if (i == j) return;
+        std::swap(va[i], va[j]);
+        std::swap(vb[i], vb[j]);
+        std::swap(w[i], w[j]);
+    };
+    ss[0] = 0;
+    es[0] = ne - 1;
+    int64_t top = 0;
+    while (top >= 0) {
+        const int64_t s = ss[top], e = es[top];
+        top--;
+        const double pv = w[s];  // selectPivotIndex always returns startIndex (:158)
+        swp(s, e);
+        int64_t low = s;
+        for (int64_t i = s; i < e; i++)
+            if (w[i] < pv) {
+                swp(i, low);
+                low++;
+            }
+        swp(low, e);
+        const int64_t pivot = low;
+        if (pivot > s + 1) {
+            if (top + 1 >= cap) return HDB_EREF_OOB;
+            ss[top + 1] = s;
+            es[top + 1] = pivot - 1;
+            top++;
+        }
+        if (pivot < e - 1) {
+            if (top + 1 >= cap) return HDB_EREF_OOB;
+            ss[top + 1] = pivot + 1;
+            es[top + 1] = e;
+            top++;
+        }
+    }
+    return HDB_OK;
+}
+
+// ------------------------------------------------------------ cluster tree
+struct Cl {
+    int32_t label, parent;
+    double birth, death = JMAX, stability = 0;
+    int32_t numPoints;
+    bool hasChildren = false;
+    std::vector<int32_t> members;  // TreeSet order
+};
+
+static int detach(Cl &c, int32_t numPoints, double level) {  // Clusters.java:39-47
+    c.numPoints -= numPoints;
+    c.stability += ((double)(numPoints + 0) * (1 / level - 1 / c.birth));
+    if (c.numPoints == 0) c.death = level;
+    else if (c.numPoints < 0) return HDB_EREF_NEGATIVE_CLUSTER;
+    return HDB_OK;
+}
+
+static uint32_t jhash(int32_t k) {
+    uint32_t h = (uint32_t)k;
+    return h ^ (h >> 16);
+}
+
+static int construct_cluster_tree(int64_t b, const int32_t *ea, const int32_t *eb, const double *ew, int64_t ne,
+                                  int32_t mcl, const int32_t *nB, std::vector<Cl> &clusters) {
+    std::vector<std::vector<int32_t>> adj(b);
+    for (int64_t i = 0; i < ne; i++) {
+        int32_t v1 = ea[i], v2 = eb[i];
+        if (v1 < 0 || v1 >= b || v2 < 0 || v2 >= b) return HDB_EREF_OOB;
+        adj[v1].push_back(v2);
+        if (v1 != v2) adj[v2].push_back(v1);
+    }
+    auto remove_first = [](std::vector<int32_t> &v, int32_t x) {
+        auto it = std::find(v.begin(), v.end(), x);
+        if (it != v.end()) v.erase(it);
+    };
+    std::vector<int32_t> label(b, 1);
+    int32_t nextLabel = 2;
+    int64_t all = 0;
+    for (int64_t i = 0; i < b; i++) all += nB[i];
+    {
+        Cl root;
+        root.label = 1;
+        root.parent = -1;
+        root.birth = NAN;
+        root.numPoints = (int32_t)all;
+        clusters.push_back(root);
+    }
+    std::vector<uint32_t> stamp(b, 0);
+    uint32_t gen = 0;
+    std::vector<int32_t> queue;
+    queue.reserve(b);
+
+    struct Aff {
+        int32_t label;
+        int64_t order;
+        std::vector<int32_t> verts;  // sorted unique (TreeSet)
+    };
+    int64_t cur = ne - 1;
+    while (cur >= 0) {
+        std::vector<Aff> aff;
+        const double cw = ew[cur];
+        while (cur >= 0 && ew[cur] == cw) {
+            const int32_t f = ea[cur], s = eb[cur];
+            remove_first(adj[f], s);
+            remove_first(adj[s], f);
+            if (label[f] == 0) {
+                cur--;
+                continue;
+            }
+            size_t k = 0;
+            for (; k < aff.size(); k++)
+                if (aff[k].label == label[f]) break;
+            if (k == aff.size()) aff.push_back(Aff{label[f], (int64_t)aff.size(), {}});
+            for (int32_t v : {f, s}) {
+                auto &vs = aff[k].verts;
+                auto it = std::lower_bound(vs.begin(), vs.end(), v);
+                if (it == vs.end() || *it != v) vs.insert(it, v);
+            }
+            cur--;
+        }
+        if (aff.empty()) continue;
+        // java.util.HashMap key iteration: bucket order, insertion order inside a bucket
+        int64_t cap = 16;
+        while ((int64_t)aff.size() > cap * 3 / 4) cap *= 2;
+        std::stable_sort(aff.begin(), aff.end(), [&](const Aff &x, const Aff &y) {
+            uint32_t bx = jhash(x.label) & (uint32_t)(cap - 1), by = jhash(y.label) & (uint32_t)(cap - 1);
+            if (bx != by) return bx < by;
+            return x.order < y.order;
+        });
+        for (auto &A : aff) {
+            const int32_t parentLabel = A.label;
+            std::vector<Cl> newc;
+            for (int32_t rootV : A.verts) {  // pollFirst over the TreeSet
+                if (++gen == 0) {
+                    std::fill(stamp.begin(), stamp.end(), 0);
+                    gen = 1;
+                }
+                queue.clear();
+                stamp[rootV] = gen;
+                queue.push_back(rootV);
+                for (size_t h = 0; h < queue.size(); h++) {
+                    int32_t v = queue[h];
+                    for (int32_t u : adj[v])
+                        if (stamp[u] != gen) {
+                            stamp[u] = gen;
+                            queue.push_back(u);
+                        }
+                }
+                int64_t countMembers = 0;
+                for (int32_t v : queue) countMembers += nB[v];
+                if (countMembers >= mcl) {
+                    Cl c;
+                    c.label = parentLabel;
+                    c.parent = parentLabel;
+                    c.birth = cw;
+                    c.numPoints = (int32_t)countMembers;
+                    c.members = queue;
+                    std::sort(c.members.begin(), c.members.end());
+                    newc.push_back(std::move(c));
+                } else {
+                    for (int32_t v : queue) label[v] = 0;
+                    for (auto &c : clusters)
+                        if (c.label == parentLabel && c.death == JMAX) {
+                            int rc = detach(c, (int32_t)countMembers, cw);
+                            if (rc) return rc;
+                            break;
+                        }
+                }
+            }
+            if (newc.size() >= 2) {
+                for (auto &c : newc) {
+                    c.label = nextLabel;
+                    for (int32_t v : c.members) label[v] = nextLabel;
+                    nextLabel++;
+                    for (auto &pc : clusters)
+                        if (pc.label == c.parent && pc.death == JMAX) {
+                            pc.hasChildren = true;
+                            int rc = detach(pc, c.numPoints, c.birth);
+                            if (rc) return rc;
+                            break;
+                        }
+                    clusters.push_back(std::move(c));
+                }
+            }
+        }
+    }
+    return HDB_OK;
+}
+
+static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *eB, const double *nnB, int64_t b,
+                          int d, int metric, int32_t *flat) {
+    // clusterTree.remove(0)
+    std::vector<Cl *> tree;
+    for (size_t i = 1; i < cl.size(); i++) tree.push_back(&cl[i]);
+    // adjListNodes: label -> list of double[5] (kept as a map in insertion-independent form)
+    struct Rec {
+        double v[5];
+    };
+    std::vector<std::vector<Rec>> adjl;
+    std::vector<int32_t> keyOf;
+    auto find_key = [&](int32_t key) -> int {
+        for (size_t i = 0; i < keyOf.size(); i++)
+            if (keyOf[i] == key) return (int)i;
+        return -1;
+    };
+    // label -> slot index (labels are small ints; dense lookup table)
+    int32_t maxlab = 1;
+    for (auto *c : tree) maxlab = std::max(maxlab, c->label);
+    std::vector<int> slot(maxlab + 2, -1);
+    auto get = [&](int32_t key) -> std::vector<Rec> * {
+        if (key < 0 || key > maxlab || slot[key] < 0) return nullptr;
+        return &adjl[slot[key]];
+    };
+    auto put = [&](int32_t key) {
+        if (key >= 0 && key <= maxlab && slot[key] < 0) {
+            slot[key] = (int)adjl.size();
+            adjl.emplace_back();
+            keyOf.push_back(key);
+        }
+    };
+    (void)find_key;
+    for (auto *par : tree) {
+        if (!par->hasChildren) put(par->label);
+        for (auto *ch : tree) {
+            if (par->label == ch->parent) {
+                put(par->label);
+                Rec r{{par->stability, (double)ch->label, ch->stability, 1.0, (double)par->parent}};
+                get(par->label)->push_back(r);
+            }
+        }
+    }
+    // Collections.sort by birth level (stable)
+    std::vector<Cl *> sorted = tree;
+    std::stable_sort(sorted.begin(), sorted.end(), [](const Cl *a, const Cl *b) { return a->birth < b->birth; });
+    for (int64_t o = 0; o < b; o++) flat[o] = 0;
+    std::vector<char> sol(maxlab + 2, 0);
+    for (auto *c : sorted) sol[c->label] = 1;
+    std::vector<char> vis(maxlab + 2, 0);
+    std::vector<int32_t> q;
+    for (auto *c : sorted) {
+        const int32_t key = c->label;
+        auto *A = get(key);
+        if (!A) return HDB_EREF_NPE;
+        double childStab = 0.0;
+        if (!A->empty()) {
+            for (auto &r : *A) childStab += r.v[2];
+            if (childStab <= (*A)[0].v[0]) {
+                for (auto &r : *A) {
+                    std::fill(vis.begin(), vis.end(), 0);
+                    int32_t rootV = (int32_t)r.v[1];
+                    q.clear();
+                    vis[rootV] = 1;
+                    q.push_back(rootV);
+                    r.v[3] = 0.0;
+                    sol[rootV] = 0;
+                    for (size_t h = 0; h < q.size(); h++) {
+                        int32_t v = q[h];
+                        auto *Av = get(v);
+                        if (Av)
+                            for (auto &rr : *Av) {
+                                sol[v] = 0;
+                                int32_t cc = (int32_t)rr.v[1];
+                                if (!vis[cc]) {
+                                    q.push_back(cc);
+                                    vis[cc] = 1;
+                                }
+                            }
+                    }
+                }
+            } else {
+                (*A)[0].v[0] = childStab;
+                auto *G = get((int32_t)(*A)[0].v[4]);
+                if (G)
+                    for (auto &rr : *G)
+                        if ((int32_t)rr.v[1] == key) rr.v[2] = childStab;
+            }
+        } else {
+            sol[key] = 0;
+        }
+    }
+    for (auto *c : sorted)
+        if (sol[c->label])
+            for (int32_t m : c->members) {
+                if (m < 0 || m >= b) return HDB_EREF_OOB;
+                flat[m] = c->label;
+            }
+    // noise -> first later-valid neighbour in index order (:485-502)
+    for (int64_t p = 0; p < b; p++) {
+        double minD = JMAX;
+        for (int64_t nb = 0; nb < b; nb++) {
+            if (p == nb) continue;
+            if (flat[p] == 0 && flat[nb] != 0) {
+                double dist = host_distance(rep + p * d, rep + nb * d, d, metric);
+                dist = host_distance_bubbles(dist, eB, nnB, p, nb);
+                if (dist < minD) {
+                    minD = dist;
+                    flat[p] = flat[nb];
+                }
+            } else if (flat[p] != 0) {
+                break;  // the condition can never hold again for this p
+            }
+        }
+    }
+    return HDB_OK;
+}
+
+int local_model_host(const double *rep, const double *eB, const double *nnB, const int32_t *nB, int64_t b, int d,
+                     int32_t min_cl_size, int metric, int32_t *mva, int32_t *mvb, double *mw, int32_t *labels,
+                     int32_t *ic_va, int32_t *ic_vb, double *ic_w, int64_t *n_ic) {
+    const int64_t ne = 2 * b - 1;
+    int rc = quicksort_edges(mva, mvb, mw, ne);
+    if (rc) return rc;
+    std::vector<Cl> cl;
+    rc = construct_cluster_tree(b, mva, mvb, mw, ne, min_cl_size, nB, cl);
+    if (rc) return rc;
+    rc = find_prominent(cl, rep, eB, nnB, b, d, metric, labels);
+    if (rc) return rc;
+    int64_t k = 0;
+    for (int64_t i = 0; i < ne; i++)
+        if (labels[mva[i]] != labels[mvb[i]]) {
+            if (ic_va) {
+                ic_va[k] = mva[i];
+                ic_vb[k] = mvb[i];
+                ic_w[k] = mw[i];
+            }
+            k++;
+        }
+    if (n_ic) *n_ic = k;
+    return HDB_OK;
+}
+
+}  // namespace hdb

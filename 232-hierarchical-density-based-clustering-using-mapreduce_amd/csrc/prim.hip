@@ -1,0 +1,491 @@
+// prim.hip -- K2: dense Prim on the mutual-reachability graph with the reference's exact
+// tie rules (HDBSCANStar.constructMST, HDBSCANStar.java:124-205; the bubble variant
+// HdbscanDataBubbles.constructMSTBubbles, HdbscanDataBubbles.java:165-254):
+//   * start at vertex n-1, best[] = Double.MAX_VALUE, parent[] = 0 (Java default);
+//   * update iff mrd < best[nb] (strict), parent = ids[cur];
+//   * select the unattached vertex with the smallest best, ties -> LARGEST index ('<=').
+// mrd = max(dist, core[cur], core[nb]) evaluated with Java's two '>' tests.
+//
+// Three launch shapes:
+//   prim_block_kernel   one workgroup per partition (n <= BS*PPT), whole Prim in-kernel,
+//                       per-step argmin = DPP/shuffle wave reduce + one LDS exchange;
+//   leaf_core_kernel    FirstStep leaf branch: cumulative core distances per partition;
+//   prim_step_kernel    large graphs: one launch per Prim step over many workgroups; each
+//                       workgroup re-reduces the previous step's per-workgroup partials
+//                       (visible across the kernel boundary), so no inter-workgroup
+//                       hand-off is needed inside a launch.  Launches are replayed from a
+//                       captured hipGraph chunk.
+// Euclidean pairs use a squared filter: s > fl(b*b)*(1+2^-50) proves sqrt(s) >= b, so
+// the exact sqrt + mrd path runs only for pairs that can improve best[nb].
+#include "internal.hpp"
+
+namespace hdb {
+
+// exact mrd for (cur, nb); returns true if it improves best
+__device__ __forceinline__ bool mrd_improves(const PrimIn &in, int64_t cur, int64_t nb, double best, double &mrd_out) {
+    const double *a = in.X + cur * in.d;
+    const double *b = in.X + nb * in.d;
+    double dist;
+    if (in.metric == HDB_METRIC_EUCLIDEAN && !in.eB) {
+        double s = sq_diff(a[0], b[0]);
+        for (int c = 1; c < in.d; c++) s = s + sq_diff(a[c], b[c]);
+        double thr = (best * best) * 1.0000000000000009;  // >= best^2 exactly
+        if (s > thr) return false;
+        dist = sqrt(s);
+    } else {
+        dist = metric_distance(a, b, in.d, in.metric);
+        if (in.eB) dist = distance_bubbles(dist, in.eB[cur], in.eB[nb], in.nnB[cur], in.nnB[nb]);
+    }
+    double mrd = dist;
+    double cc = in.core[cur], cn = in.core[nb];
+    if (cc > mrd) mrd = cc;
+    if (cn > mrd) mrd = cn;
+    mrd_out = mrd;
+    return mrd < best;
+}
+
+__device__ __forceinline__ void wave_argmin_last(double &v, int &i) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        double v2 = __shfl_xor(v, off);
+        int i2 = __shfl_xor(i, off);
+        argmin_last(v, i, v2, i2);
+    }
+}
+
+// ---------------------------------------------------------- block kernel
+// parts: partition list for this launch (indices into offsets); vertex rows of partition
+// p are [offsets[p], offsets[p+1]).  Edges at eoff[p].
+template <int BS, int PPT>
+__global__ __launch_bounds__(BS) void prim_block_kernel(PrimIn in, const int64_t *__restrict__ offsets,
+                                                        const int64_t *__restrict__ eoff,
+                                                        const int32_t *__restrict__ parts, int self_edges,
+                                                        int32_t *__restrict__ va, int32_t *__restrict__ vb,
+                                                        double *__restrict__ w) {
+    constexpr int NW = BS / 64;
+    __shared__ double s_v[2][NW];
+    __shared__ int s_i[2][NW];
+    const int p = parts[blockIdx.x];
+    const int64_t o = offsets[p];
+    const int n = (int)(offsets[p + 1] - o);
+    if (n <= 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    PrimIn L = in;
+    L.X = in.X + o * in.d;
+    L.core = in.core + o;
+    L.ids = in.ids + o;
+    if (in.eB) {
+        L.eB = in.eB + o;
+        L.nnB = in.nnB + o;
+    }
+    double best[PPT];
+    int par[PPT];
+    unsigned att = 0;
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        best[k] = JMAX;
+        par[k] = 0;
+        int i = tid + k * BS;
+        if (i == n - 1 || i >= n) att |= 1u << k;
+    }
+    int cur = n - 1;
+    for (int step = 1; step < n; step++) {
+        double lv = INFINITY;
+        int li = -1;
+        const int cid = L.ids[cur];
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            if (att & (1u << k)) continue;
+            int i = tid + k * BS;
+            double mrd;
+            if (mrd_improves(L, cur, i, best[k], mrd)) {
+                best[k] = mrd;
+                par[k] = cid;
+            }
+            argmin_last(lv, li, best[k], i);
+        }
+        wave_argmin_last(lv, li);
+        if (NW > 1) {
+            const int buf = step & 1;
+            if (lane == 0) {
+                s_v[buf][wid] = lv;
+                s_i[buf][wid] = li;
+            }
+            __syncthreads();
+            lv = s_v[buf][0];
+            li = s_i[buf][0];
+#pragma unroll
+            for (int q = 1; q < NW; q++) argmin_last(lv, li, s_v[buf][q], s_i[buf][q]);
+        }
+        cur = li;  // uniform
+        if (cur < 0) break;  // unreachable: an unattached vertex always exists
+        if ((cur % BS) == tid) att |= 1u << (cur / BS);
+    }
+    const int64_t eo = eoff[p];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        int i = tid + k * BS;
+        if (i < n - 1) {
+            va[eo + i] = par[k];
+            vb[eo + i] = L.ids[i];
+            w[eo + i] = best[k];
+        }
+        if (self_edges && i < n) {
+            va[eo + n - 1 + i] = L.ids[i];
+            vb[eo + n - 1 + i] = L.ids[i];
+            w[eo + n - 1 + i] = L.core[i];
+        }
+    }
+}
+
+// ------------------------------------------------- leaf cumulative cores
+// HDBSCANStar.calculateCoreDistances inside a leaf partition (HDBSCANStar.java:79-103):
+// per-row top-KC lists (self included, values as Java computes them), then the
+// never-reset buffer = prefix merge over rows in row order (one lane).  KC >= K; the
+// K-th smallest of a union is element K-1 of its top-KC.
+template <int KC>
+__device__ __forceinline__ void ins_kc(double (&buf)[KC], double x) {
+    if (!(x < buf[KC - 1])) return;
+#pragma unroll
+    for (int i = 0; i < KC; i++) {
+        double b = buf[i];
+        bool lt = x < b;
+        buf[i] = lt ? x : b;
+        x = lt ? b : x;
+    }
+}
+
+template <int BS, int KC>
+__global__ __launch_bounds__(BS) void leaf_core_kernel(const double *__restrict__ X, int d, int metric,
+                                                       const int64_t *__restrict__ offsets,
+                                                       const int32_t *__restrict__ parts, int K,
+                                                       double *__restrict__ lists /* rows*KC */,
+                                                       double *__restrict__ core) {
+    const int p = parts[blockIdx.x];
+    const int64_t o = offsets[p];
+    const int n = (int)(offsets[p + 1] - o);
+    for (int i = threadIdx.x; i < n; i += BS) {
+        double buf[KC];
+#pragma unroll
+        for (int k = 0; k < KC; k++) buf[k] = JMAX;
+        const double *xi = X + (o + i) * d;
+        for (int j = 0; j < n; j++) ins_kc<KC>(buf, metric_distance(xi, X + (o + j) * d, d, metric));
+#pragma unroll
+        for (int k = 0; k < KC; k++) lists[(o + i) * KC + k] = buf[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double buf[KC];
+#pragma unroll
+        for (int k = 0; k < KC; k++) buf[k] = JMAX;
+        for (int i = 0; i < n; i++) {
+#pragma unroll
+            for (int k = 0; k < KC; k++) ins_kc<KC>(buf, lists[(o + i) * KC + k]);
+            double c = buf[0];
+#pragma unroll
+            for (int k = 1; k < KC; k++)
+                if (k == K - 1) c = buf[k];
+            core[o + i] = c;
+        }
+    }
+}
+
+void leaf_cores_device(hdb_ctx *ctx, const double *X, int d, int metric, int P, const int64_t *d_off,
+                       const int32_t *d_parts, int np, int64_t total_rows, int K, double *core) {
+    if (np == 0) return;
+    int KC = K <= 3 ? 3 : (K <= 7 ? 7 : (K <= 15 ? 15 : 31));
+    if (K > 31) HDB_THROW(HDB_EINVAL, "minPts too large (max 32)");
+    double *lists = (double *)arena(ctx, A_WORK2, sizeof(double) * (size_t)std::max<int64_t>(total_rows, 1) * KC);
+    KernelTimer t(ctx, "leaf_core");
+    switch (KC) {
+    case 3: hipLaunchKernelGGL((leaf_core_kernel<256, 3>), dim3(np), dim3(256), 0, ctx->stream, X, d, metric, d_off, d_parts, K, lists, core); break;
+    case 7: hipLaunchKernelGGL((leaf_core_kernel<256, 7>), dim3(np), dim3(256), 0, ctx->stream, X, d, metric, d_off, d_parts, K, lists, core); break;
+    case 15: hipLaunchKernelGGL((leaf_core_kernel<256, 15>), dim3(np), dim3(256), 0, ctx->stream, X, d, metric, d_off, d_parts, K, lists, core); break;
+    default: hipLaunchKernelGGL((leaf_core_kernel<256, 31>), dim3(np), dim3(256), 0, ctx->stream, X, d, metric, d_off, d_parts, K, lists, core); break;
+    }
+    HIP_CHECK(hipGetLastError());
+    (void)P;
+}
+
+// ------------------------------------------------------ stepwise kernel
+// State per partition (global): best[], par[], att[] over its vertices; partials
+// [2][nwg_p] (value, index) double-buffered by step parity; step counter ctr[2].
+struct StepState {
+    double *best;
+    int32_t *par;
+    uint8_t *att;
+    double *pv;     // [2][total_wg]
+    int32_t *pidx;  // [2][total_wg]
+    int32_t *cur0;  // start vertex per partition (n-1)
+};
+
+// Block b belongs to partition wg_part[b]; its local index within the partition's
+// workgroups is b - wg_first[p]; partition p has wg_count[p] workgroups.
+template <int BS, int PPT>
+__global__ __launch_bounds__(BS) void prim_step_kernel(PrimIn in, const int64_t *__restrict__ offsets,
+                                                       const int32_t *__restrict__ wg_part,
+                                                       const int32_t *__restrict__ wg_first,
+                                                       const int32_t *__restrict__ wg_count, StepState st,
+                                                       int step, int parity) {
+    constexpr int NW = BS / 64;
+    __shared__ double s_v[NW];
+    __shared__ int s_i[NW];
+    __shared__ int s_cur;
+    const int b = blockIdx.x;
+    const int p = wg_part[b];
+    const int64_t o = offsets[p];
+    const int n = (int)(offsets[p + 1] - o);
+    if (step >= n) return;  // this partition is done
+    const int first = wg_first[p], cnt = wg_count[p];
+    const int lb = b - first;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+    // current vertex: reduce the previous step's partials (or the start vertex)
+    int cur;
+    if (step == 1) {
+        cur = n - 1;
+    } else {
+        if (tid < 64) {
+            double v = INFINITY;
+            int i = -1;
+            for (int q = lane; q < cnt; q += 64)
+                argmin_last(v, i, st.pv[(parity ^ 1) * gridDim.x + first + q], st.pidx[(parity ^ 1) * gridDim.x + first + q]);
+            wave_argmin_last(v, i);
+            if (lane == 0) s_cur = i;
+        }
+        __syncthreads();
+        cur = s_cur;
+        if (cur < 0) return;
+    }
+    PrimIn L = in;
+    L.X = in.X + o * in.d;
+    L.core = in.core + o;
+    L.ids = in.ids + o;
+    if (in.eB) {
+        L.eB = in.eB + o;
+        L.nnB = in.nnB + o;
+    }
+    // mark cur attached (owner workgroup), skip it below
+    const int per_wg = BS * PPT;
+    const int base = lb * per_wg;
+    double lv = INFINITY;
+    int li = -1;
+    const int cid = L.ids[cur];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        int i = base + tid + k * BS;
+        if (i >= n) continue;
+        const int64_t gi = o + i;
+        if (i == cur) {
+            st.att[gi] = 1;
+            continue;
+        }
+        if (st.att[gi]) continue;
+        double bst = st.best[gi];
+        double mrd;
+        if (mrd_improves(L, cur, i, bst, mrd)) {
+            bst = mrd;
+            st.best[gi] = mrd;
+            st.par[gi] = cid;
+        }
+        argmin_last(lv, li, bst, i);
+    }
+    wave_argmin_last(lv, li);
+    if (lane == 0) {
+        s_v[wid] = lv;
+        s_i[wid] = li;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double v = s_v[0];
+        int i = s_i[0];
+        for (int q = 1; q < NW; q++) argmin_last(v, i, s_v[q], s_i[q]);
+        st.pv[parity * gridDim.x + b] = v;
+        st.pidx[parity * gridDim.x + b] = i;
+    }
+}
+
+__global__ void prim_step_init_kernel(const int64_t *__restrict__ offsets, int P, double *best, int32_t *par,
+                                      uint8_t *att, int64_t total) {
+    HDB_GRID_STRIDE(g, total) {
+        best[g] = JMAX;
+        par[g] = 0;
+        att[g] = 0;
+    }
+}
+
+__global__ void prim_step_final_kernel(PrimIn in, const int64_t *__restrict__ offsets,
+                                       const int64_t *__restrict__ eoff, int P, StepState st, int self_edges,
+                                       int32_t *__restrict__ va, int32_t *__restrict__ vb, double *__restrict__ w) {
+    // one block per partition
+    const int p = blockIdx.x;
+    const int64_t o = offsets[p];
+    const int n = (int)(offsets[p + 1] - o);
+    const int64_t eo = eoff[p];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        if (i < n - 1) {
+            va[eo + i] = st.par[o + i];
+            vb[eo + i] = in.ids[o + i];
+            w[eo + i] = st.best[o + i];
+        }
+        if (self_edges) {
+            va[eo + n - 1 + i] = in.ids[o + i];
+            vb[eo + n - 1 + i] = in.ids[o + i];
+            w[eo + n - 1 + i] = in.core[o + i];
+        }
+    }
+}
+
+// ------------------------------------------------------------------ host
+template <int BS, int PPT>
+static void launch_block(hdb_ctx *ctx, const PrimIn &in, const int64_t *offs, const int64_t *eoff,
+                         const int32_t *parts, int np, int self_edges, int32_t *va, int32_t *vb, double *w) {
+    if (np == 0) return;
+    KernelTimer t(ctx, "prim_block");
+    hipLaunchKernelGGL((prim_block_kernel<BS, PPT>), dim3(np), dim3(BS), 0, ctx->stream, in, offs, eoff, parts,
+                       self_edges, va, vb, w);
+    HIP_CHECK(hipGetLastError());
+}
+
+// size classes for the block kernel
+static int block_class(int64_t n) {
+    if (n <= 64) return 0;        // 64 x 1
+    if (n <= 256) return 1;       // 64 x 4
+    if (n <= 1024) return 2;      // 256 x 4
+    if (n <= 4096) return 3;      // 1024 x 4
+    return 4;                     // stepwise
+}
+
+// Batched Prim. Device pointers: X (rows), offsets (P+1, host copy h_offs), core, ids.
+void prim_batched_device(hdb_ctx *ctx, const PrimIn &in, const int64_t *h_offs, int P, int self_edges,
+                         int32_t *va, int32_t *vb, double *w) {
+    // edge offsets + per-class partition lists (host side), then upload
+    std::vector<int64_t> eoff(P + 1, 0);
+    std::vector<int32_t> cls[5];
+    int64_t total_v = h_offs[P] - h_offs[0];
+    for (int p = 0; p < P; p++) {
+        int64_t n = h_offs[p + 1] - h_offs[p];
+        if (n < 0) HDB_THROW(HDB_EINVAL, "offsets must be non-decreasing");
+        eoff[p + 1] = eoff[p] + (n > 0 ? (n - 1) + (self_edges ? n : 0) : 0);
+        if (n > 0) cls[block_class(n)].push_back(p);
+    }
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+        size_t o = off;
+        off += (bytes + 255) & ~size_t(255);
+        return o;
+    };
+    size_t o_off = carve(sizeof(int64_t) * (P + 1)), o_eoff = carve(sizeof(int64_t) * (P + 1));
+    size_t o_parts = carve(sizeof(int32_t) * (P + 1));
+    // stepwise state
+    std::vector<int32_t> wg_part, wg_first(P, 0), wg_count(P, 0);
+    constexpr int SBS = 256, SPPT = 4;
+    for (int32_t p : cls[4]) {
+        int64_t n = h_offs[p + 1] - h_offs[p];
+        int c = (int)ceil_div(n, SBS * SPPT);
+        wg_first[p] = (int)wg_part.size();
+        wg_count[p] = c;
+        for (int q = 0; q < c; q++) wg_part.push_back(p);
+    }
+    int nwg = (int)wg_part.size();
+    size_t o_wgp = carve(sizeof(int32_t) * (nwg + 1)), o_wgf = carve(sizeof(int32_t) * (P + 1)),
+           o_wgc = carve(sizeof(int32_t) * (P + 1));
+    size_t o_best = 0, o_par = 0, o_att = 0, o_pv = 0, o_pi = 0;
+    if (nwg) {
+        o_best = carve(sizeof(double) * total_v);
+        o_par = carve(sizeof(int32_t) * total_v);
+        o_att = carve(total_v);
+        o_pv = carve(sizeof(double) * 2 * nwg);
+        o_pi = carve(sizeof(int32_t) * 2 * nwg);
+    }
+    char *base = (char *)arena(ctx, A_WORK1, off);
+    int64_t *d_off = (int64_t *)(base + o_off), *d_eoff = (int64_t *)(base + o_eoff);
+    int32_t *d_parts = (int32_t *)(base + o_parts);
+    std::vector<int64_t> rel(P + 1);
+    for (int p = 0; p <= P; p++) rel[p] = h_offs[p] - h_offs[0];
+    HIP_CHECK(hipMemcpyAsync(d_off, rel.data(), sizeof(int64_t) * (P + 1), hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipMemcpyAsync(d_eoff, eoff.data(), sizeof(int64_t) * (P + 1), hipMemcpyHostToDevice, ctx->stream));
+    std::vector<int32_t> plist;
+    int cstart[5];
+    for (int c = 0; c < 5; c++) {
+        cstart[c] = (int)plist.size();
+        plist.insert(plist.end(), cls[c].begin(), cls[c].end());
+    }
+    if (!plist.empty())
+        HIP_CHECK(hipMemcpyAsync(d_parts, plist.data(), sizeof(int32_t) * plist.size(), hipMemcpyHostToDevice,
+                                 ctx->stream));
+    launch_block<64, 1>(ctx, in, d_off, d_eoff, d_parts + cstart[0], (int)cls[0].size(), self_edges, va, vb, w);
+    launch_block<64, 4>(ctx, in, d_off, d_eoff, d_parts + cstart[1], (int)cls[1].size(), self_edges, va, vb, w);
+    launch_block<256, 4>(ctx, in, d_off, d_eoff, d_parts + cstart[2], (int)cls[2].size(), self_edges, va, vb, w);
+    launch_block<1024, 4>(ctx, in, d_off, d_eoff, d_parts + cstart[3], (int)cls[3].size(), self_edges, va, vb, w);
+    if (nwg) {
+        int32_t *d_wgp = (int32_t *)(base + o_wgp), *d_wgf = (int32_t *)(base + o_wgf),
+                *d_wgc = (int32_t *)(base + o_wgc);
+        HIP_CHECK(hipMemcpyAsync(d_wgp, wg_part.data(), sizeof(int32_t) * nwg, hipMemcpyHostToDevice, ctx->stream));
+        HIP_CHECK(hipMemcpyAsync(d_wgf, wg_first.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, ctx->stream));
+        HIP_CHECK(hipMemcpyAsync(d_wgc, wg_count.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, ctx->stream));
+        StepState st;
+        st.best = (double *)(base + o_best);
+        st.par = (int32_t *)(base + o_par);
+        st.att = (uint8_t *)(base + o_att);
+        st.pv = (double *)(base + o_pv);
+        st.pidx = (int32_t *)(base + o_pi);
+        st.cur0 = nullptr;
+        hipLaunchKernelGGL(prim_step_init_kernel, dim3(1024), dim3(256), 0, ctx->stream, d_off, P, st.best, st.par,
+                           st.att, total_v);
+        int64_t maxn = 0;
+        for (int32_t p : cls[4]) maxn = std::max(maxn, h_offs[p + 1] - h_offs[p]);
+        // steps 1..maxn-1; chunks captured into a hipGraph and replayed
+        const int CH = 256;
+        hipGraphExec_t exec = nullptr;
+        KernelTimer t(ctx, "prim_step_total");
+        int step = 1;
+        // eager for the first partial chunk so the graph chunk starts at an odd step
+        auto launch_one = [&](int s) {
+            hipLaunchKernelGGL((prim_step_kernel<SBS, SPPT>), dim3(nwg), dim3(SBS), 0, ctx->stream, in, d_off, d_wgp,
+                               d_wgf, d_wgc, st, s, s & 1);
+        };
+        while (step < maxn) {
+            int remain = (int)(maxn - step);
+            if (remain < CH || ctx->timing) {
+                for (int s = 0; s < std::min(remain, CH); s++) launch_one(step + s);
+                HIP_CHECK(hipGetLastError());
+                step += std::min(remain, CH);
+                continue;
+            }
+            // capture CH launches with absolute steps; re-capture per chunk (steps are args)
+            hipGraph_t graph;
+            HIP_CHECK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+            for (int s = 0; s < CH; s++) launch_one(step + s);
+            HIP_CHECK(hipStreamEndCapture(ctx->stream, &graph));
+            if (!exec) {
+                HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+            } else {
+                hipGraphExecUpdateResult res;
+                hipGraphNode_t errn;
+                if (hipGraphExecUpdate(exec, graph, &errn, &res) != hipSuccess) {
+                    (void)hipGetLastError();
+                    HIP_CHECK(hipGraphExecDestroy(exec));
+                    HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+                }
+            }
+            HIP_CHECK(hipGraphLaunch(exec, ctx->stream));
+            HIP_CHECK(hipGraphDestroy(graph));
+            step += CH;
+        }
+        if (exec) {
+            HIP_CHECK(hipStreamSynchronize(ctx->stream));
+            HIP_CHECK(hipGraphExecDestroy(exec));
+        }
+        // edges for stepwise partitions
+        std::vector<int32_t> big(cls[4].begin(), cls[4].end());
+        for (int32_t p : big) {
+            // one block per partition via a shifted offsets view
+            hipLaunchKernelGGL(prim_step_final_kernel, dim3(1), dim3(256), 0, ctx->stream, in, d_off + p, d_eoff + p, 1,
+                               st, self_edges, va, vb, w);
+        }
+        HIP_CHECK(hipGetLastError());
+    }
+}
+
+}  // namespace hdb

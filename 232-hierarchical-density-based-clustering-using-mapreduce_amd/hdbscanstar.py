@@ -1,0 +1,192 @@
+"""Mirror of the reference's ``distance`` and ``hdbscanstar`` packages over libhdbmi.
+
+Same class/method names and argument meaning as the Java (源代码/distance/*.java,
+源代码/hdbscanstar/HDBSCANStar.java, UndirectedGraph.java); the bodies call the C-ABI.
+Arrays may be numpy (host) or torch tensors (host or HIP device); results come back on the
+side the input lives on.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _capi as A
+
+
+# --------------------------------------------------------------- distance
+class DistanceCalculator:
+    """distance/DistanceCalculator.java:9-21."""
+
+    name = ""
+
+    def getName(self) -> str:  # DistanceCalculator.java:20
+        return self.name
+
+    def computeDistance(self, attributesOne, attributesTwo) -> float:  # :17
+        a = np.asarray(attributesOne, np.float64).reshape(1, -1)
+        b = np.asarray(attributesTwo, np.float64).reshape(1, -1)
+        return float(distance_rows(a, b, self)[0])
+
+    @property
+    def metric(self) -> int:
+        return A.METRIC[self.getName()]
+
+
+class EuclideanDistance(DistanceCalculator):
+    name = "euclidean"  # EuclideanDistance.java:28-41
+
+
+class CosineSimilarity(DistanceCalculator):
+    name = "cosine"  # CosineSimilarity.java:28-45
+
+
+class PearsonCorrelation(DistanceCalculator):
+    name = "pearson"  # PearsonCorrelation.java:28-56
+
+
+class ManhattanDistance(DistanceCalculator):
+    name = "manhattan"  # ManhattanDistance.java:28-41
+
+
+class SupremumDistance(DistanceCalculator):
+    name = "supremum"  # SupremumDistance.java:28-43
+
+
+def metric_of(distanceFunction) -> int:
+    if distanceFunction is None:
+        return 0
+    if isinstance(distanceFunction, str):
+        return A.METRIC[distanceFunction]
+    if isinstance(distanceFunction, int):
+        return distanceFunction
+    return A.METRIC[distanceFunction.getName()]
+
+
+def _ctx(ref: A.Arr, ctx=None) -> A.Context:
+    if ctx is not None:
+        return ctx
+    dev = ref.device.index if (ref.device is not None and ref.device.type == "cuda") else 0
+    c = A.Context.get(dev or 0)
+    if ref.device is not None and ref.device.type == "cuda":
+        c.use_torch_stream()
+    return c
+
+
+def distance_rows(a, b, distanceFunction=None, ctx=None):
+    aa, bb = A.Arr(a, np.float64), A.Arr(b, np.float64)
+    n, d = aa.obj.shape
+    out = A.new_like(aa, (n,), np.float64)
+    c = _ctx(aa, ctx)
+    A.check(A.lib().hdb_distance_rows(c.h, aa.p, bb.p, n, d, metric_of(distanceFunction), A.ptr(out)),
+            "hdb_distance_rows")
+    return out
+
+
+# ---------------------------------------------------------- UndirectedGraph
+class UndirectedGraph:
+    """hdbscanstar/UndirectedGraph.java: parallel edge arrays (+ adjacency on demand)."""
+
+    def __init__(self, verticesA, verticesB, edgeWeights, numVertices: int | None = None):
+        self.verticesA = verticesA
+        self.verticesB = verticesB
+        self.edgeWeights = edgeWeights
+        self.numVertices = numVertices
+
+    def _host(self):
+        def h(x, dt):
+            if A.is_torch(x):
+                return np.ascontiguousarray(x.detach().cpu().numpy(), dtype=dt)
+            return np.ascontiguousarray(x, dtype=dt)
+        return h(self.verticesA, np.int32), h(self.verticesB, np.int32), h(self.edgeWeights, np.float64)
+
+    def quicksortByEdgeWeight(self):
+        """UndirectedGraph.java:93-124 (pivot = startIndex quirk), in place on host copies."""
+        a, b, w = self._host()
+        A.check(A.lib().hdb_quicksort_edges(A.ptr(a), A.ptr(b), A.ptr(w), w.shape[0]), "quicksortByEdgeWeight")
+        self.verticesA, self.verticesB, self.edgeWeights = a, b, w
+
+    def getNumVertices(self):
+        return self.numVertices
+
+    def getNumEdges(self):
+        return int(self.edgeWeights.shape[0])
+
+    def getFirstVertexAtIndex(self, i):
+        return int(self.verticesA[i])
+
+    def getSecondVertexAtIndex(self, i):
+        return int(self.verticesB[i])
+
+    def getEdgeWeightAtIndex(self, i):
+        return float(self.edgeWeights[i])
+
+    def getVerticeA(self):
+        return self.verticesA
+
+    def getVericeB(self):  # sic, UndirectedGraph.java:259
+        return self.verticesB
+
+    def getEges(self):  # sic, UndirectedGraph.java:263
+        return self.edgeWeights
+
+
+# --------------------------------------------------------------- HDBSCANStar
+class HDBSCANStar:
+    """hdbscanstar/HDBSCANStar.java -- the hot-path entry points."""
+
+    def __init__(self, ctx: A.Context | None = None):
+        self.ctx = ctx
+
+    def calculateCoreDistances(self, dataSet, k: int, distanceFunction=None,
+                               semantics: int = A.CORE_INCL_SELF_CUMULATIVE):
+        """HDBSCANStar.java:71-106 (live: the k-NN buffer is never reset between points).
+        semantics selects the reference's other variants (CORE_INCL_SELF:
+        CoreDistanceMapper.java:71-109, CORE_EXCL_SELF: CreateLocalMST.java:138-185)."""
+        X = A.Arr(dataSet, np.float64)
+        n, d = X.obj.shape
+        core = A.new_like(X, (n,), np.float64)
+        c = _ctx(X, self.ctx)
+        A.check(A.lib().hdb_core_distances(c.h, X.p, n, d, k, metric_of(distanceFunction), semantics,
+                                           A.ptr(core)), "calculateCoreDistances")
+        return core
+
+    def constructMST(self, dataSet, coreDistances, selfEdges: bool, distanceFunction=None, indices=None,
+                     totalLength=None) -> UndirectedGraph:
+        """HDBSCANStar.java:124-205 -- exact reference Prim (totalLength unused, as in Java)."""
+        X = A.Arr(dataSet, np.float64)
+        n, d = X.obj.shape
+        core = A.Arr(coreDistances, np.float64)
+        ids = A.Arr(indices, np.int32) if indices is not None else None
+        ne = (n - 1) + (n if selfEdges else 0)
+        va = A.new_like(X, (ne,), np.int32)
+        vb = A.new_like(X, (ne,), np.int32)
+        w = A.new_like(X, (ne,), np.float64)
+        c = _ctx(X, self.ctx)
+        A.check(A.lib().hdb_prim_mst(c.h, X.p, n, d, core.p, ids.p if ids else None, metric_of(distanceFunction),
+                                     int(bool(selfEdges)), A.ptr(va), A.ptr(vb), A.ptr(w)), "constructMST")
+        return UndirectedGraph(va, vb, w)
+
+    def constructMSTBoruvka(self, dataSet, coreDistances, selfEdges: bool, distanceFunction=None) -> UndirectedGraph:
+        """Large-graph MST (K2b): same sorted weights as constructMST, ties broken by
+        (w, min id, max id); edges sorted by that key, then the self edges."""
+        X = A.Arr(dataSet, np.float64)
+        n, d = X.obj.shape
+        core = A.Arr(coreDistances, np.float64)
+        ne = (n - 1) + (n if selfEdges else 0)
+        va = A.new_like(X, (ne,), np.int32)
+        vb = A.new_like(X, (ne,), np.int32)
+        w = A.new_like(X, (ne,), np.float64)
+        c = _ctx(X, self.ctx)
+        A.check(A.lib().hdb_mst_boruvka(c.h, X.p, n, d, core.p, metric_of(distanceFunction), int(bool(selfEdges)),
+                                        A.ptr(va), A.ptr(vb), A.ptr(w)), "constructMSTBoruvka")
+        return UndirectedGraph(va, vb, w)
+
+    def knn(self, dataSet, k: int, distanceFunction=None, exclSelf: bool = False, withIndices: bool = False):
+        """Per-row k smallest distances (ascending, Double.MAX_VALUE padded) [+ indices]."""
+        X = A.Arr(dataSet, np.float64)
+        n, d = X.obj.shape
+        dist = A.new_like(X, (n, k), np.float64)
+        idx = A.new_like(X, (n, k), np.int32) if withIndices else None
+        c = _ctx(X, self.ctx)
+        A.check(A.lib().hdb_knn(c.h, X.p, n, d, k, metric_of(distanceFunction), int(exclSelf), A.ptr(dist),
+                                A.ptr(idx)), "knn")
+        return (dist, idx) if withIndices else dist

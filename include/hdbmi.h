@@ -1,0 +1,166 @@
+/*
+ * hdbmi.h -- C-ABI of the MI355X-native MR-HDBSCAN* hot path.
+ *
+ * The reference (SZU-AdvTech-2022/232, Java 8 + Spark 2.x) keeps its driver and operator
+ * surface; each entry point below is the body a JNI shim substitutes for the Java method
+ * cited next to it (see INTEGRATION.md for the binding).  Plain C types only.
+ *
+ * Memory: every array argument may be HOST memory or DEVICE memory of the context's
+ * device (detected per pointer).  Host inputs are staged to HBM on the context stream and
+ * host outputs copied back before the call returns (PCIe-inclusive).  When every pointer
+ * is device memory the call is stream-ordered on the context stream and returns without
+ * synchronising (except where noted).  The caller allocates every output; the library
+ * never retains a caller pointer after return.
+ *
+ * Errors: int status, 0 = OK, < 0 = error; hdb_last_error() returns a thread-local message.
+ * The HDB_EREF_* codes reproduce the reference's own exceptions (a JNI shim maps them to
+ * the corresponding Java RuntimeException).
+ *
+ * Threading: re-entrant; use one hdb_ctx per calling thread.
+ */
+#ifndef HDBMI_H
+#define HDBMI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HDB_OK 0
+#define HDB_EINVAL (-1)
+#define HDB_EDEVICE (-2)
+#define HDB_ENOMEM (-3)
+#define HDB_EREF_NPE (-10)              /* java.lang.NullPointerException                    */
+#define HDB_EREF_OOB (-11)              /* java.lang.ArrayIndexOutOfBoundsException          */
+#define HDB_EREF_NEGATIVE_CLUSTER (-12) /* Clusters.java:45-46 "Cluster cannot have less than 0 points." */
+#define HDB_EREF_DIVZERO (-13)          /* java.lang.ArithmeticException: / by zero          */
+
+/* DistanceCalculator.getName() (distance/DistanceCalculator.java:20) */
+#define HDB_METRIC_EUCLIDEAN 0 /* EuclideanDistance.java:28-36  */
+#define HDB_METRIC_COSINE 1    /* CosineSimilarity.java:28-40   */
+#define HDB_METRIC_PEARSON 2   /* PearsonCorrelation.java:28-51 */
+#define HDB_METRIC_MANHATTAN 3 /* ManhattanDistance.java:28-36  */
+#define HDB_METRIC_SUPREMUM 4  /* SupremumDistance.java:28-38   */
+
+/* Core-distance semantics present in the reference */
+#define HDB_CORE_INCL_SELF_CUMULATIVE 0 /* HDBSCANStar.java:71-106 (live; buffer never reset) */
+#define HDB_CORE_INCL_SELF 1            /* CoreDistanceMapper.java:71-109                      */
+#define HDB_CORE_EXCL_SELF 2            /* CreateLocalMST.java:138-185 (standard HDBSCAN*)     */
+
+/* Bubble-statistics variants */
+#define HDB_BUBBLE_COMBINESTEP 0 /* mappers/CombineStep.java:18-64 (live)            */
+#define HDB_BUBBLE_CF 1          /* datastructure/ClusterFeatureDataBubbles.java:192-215 */
+
+typedef struct hdb_ctx hdb_ctx;
+
+/* ------------------------------------------------------------------ context */
+int hdb_ctx_create(int device, hdb_ctx **out);
+void hdb_ctx_destroy(hdb_ctx *ctx);
+/* Run on a caller-owned hipStream_t (e.g. torch's current stream); NULL = context-owned. */
+int hdb_ctx_set_stream(hdb_ctx *ctx, void *hip_stream);
+/* Per-kernel HIP-event timing (off by default). */
+int hdb_ctx_set_timing(hdb_ctx *ctx, int enable);
+/* Synchronises, returns the summed device time (ms) and launch count of kernel `name`
+ * since the last reset, then resets that accumulator when reset != 0. */
+int hdb_ctx_kernel_time(hdb_ctx *ctx, const char *name, double *ms_total, int64_t *launches, int reset);
+int hdb_ctx_synchronize(hdb_ctx *ctx);
+const char *hdb_last_error(void);
+int hdb_version(void);
+
+/* ------------------------------------------------------- distance (a1, a2) */
+/* Pairwise distance of rows a[i] and b[i], i < n -- DistanceCalculator.computeDistance. */
+int hdb_distance_rows(hdb_ctx *ctx, const double *a, const double *b, int64_t n, int32_t d, int32_t metric,
+                      double *out);
+
+/* ------------------------------------------------------ core distances (a3, a4)
+ * Replaces HDBSCANStar.calculateCoreDistances(double[][] dataSet, int k, DistanceCalculator)
+ * (HDBSCANStar.java:71) and its variants CreateLocalMST.java:138 / CoreDistanceMapper.java:71.
+ * X: n x d row-major doubles.  core_out: n doubles. */
+int hdb_core_distances(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t min_pts, int32_t metric,
+                       int32_t semantics, double *core_out);
+
+/* Per-row k smallest distances, ascending (Double.MAX_VALUE padded), optional neighbour
+ * indices.  The value lists are the kernel output every core semantics derives from. */
+int hdb_knn(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t k, int32_t metric, int32_t excl_self,
+            double *dist_out /* n*k */, int32_t *idx_out /* n*k, nullable */);
+
+/* ----------------------------------------------------------------- MST (a5, a6)
+ * Replaces HDBSCANStar.constructMST(double[][] dataSet, double[] coreDistances, boolean
+ * selfEdges, DistanceCalculator, int[] indices, int totalLength) (HDBSCANStar.java:124-125).
+ * Exact reference Prim: start vertex n-1, strict '<' update, '<=' select, Double.MAX_VALUE
+ * init.  Edge i < n-1 = (va=parent of i, vb=ids[i], w); then n self edges if self_edges.
+ * ids nullable (identity). */
+int hdb_prim_mst(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const double *core, const int32_t *ids,
+                 int32_t metric, int32_t self_edges, int32_t *va, int32_t *vb, double *w);
+
+/* The same Prim for P independent partitions stored back to back: partition p = rows
+ * offsets[p] .. offsets[p+1]-1 of X/core/ids.  Edges of partition p start at
+ * edge_offsets[p] = sum_{q<p} (n_q - 1 + (self_edges ? n_q : 0)). */
+int hdb_prim_mst_batched(hdb_ctx *ctx, const double *X, const int64_t *offsets, int32_t P, int32_t d,
+                         const double *core, const int32_t *ids, int32_t metric, int32_t self_edges, int32_t *va,
+                         int32_t *vb, double *w);
+
+/* FirstStep.call leaf branch (mappers/FirstStep.java:104-120) for P partitions at once:
+ * live cumulative core distances (HDBSCANStar.java:71-106) + Prim with self edges, vertex
+ * ids = global point ids.  core_out nullable. */
+int hdb_leaf_msts(hdb_ctx *ctx, const double *X, const int64_t *offsets, int32_t P, int32_t d, const int32_t *ids,
+                  int32_t min_pts, int32_t metric, double *core_out, int32_t *va, int32_t *vb, double *w);
+
+/* Exact minimum spanning tree of the mutual-reachability graph for large n (Boruvka,
+ * K2b).  Any MST: the sorted weight sequence equals the reference Prim's exactly; the
+ * topology can differ only among equal-weight edges (ties broken by (w, min id, max id)).
+ * Outputs n-1 edges (va < vb, by the library's order), then n self edges if self_edges. */
+int hdb_mst_boruvka(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const double *core, int32_t metric,
+                    int32_t self_edges, int32_t *va, int32_t *vb, double *w);
+
+/* ---------------------------------------------------------- nearest sample (a8, a9)
+ * FirstStep.call non-leaf branch (FirstStep.java:74-85): the FIRST minimum over the sample
+ * list (strict '<').  With x_key/s_key non-NULL only samples of the point's key are scanned
+ * (D3; ClusterFeaturesByNodesMapper.java:53-61).  nearest_out = list position (0 if no
+ * candidate, as the Java init), dist_out nullable (Double.MAX_VALUE if none). */
+int hdb_nearest_sample(hdb_ctx *ctx, const double *X, int64_t n, const double *S, int64_t m, int32_t d,
+                       int32_t metric, const int32_t *x_key, const int32_t *s_key, int32_t *nearest_out,
+                       double *dist_out);
+
+/* --------------------------------------------------------- bubble statistics (a11, a12)
+ * Bulk CombineStep (CombineStep.java:18-64) over a partition: member order = ascending
+ * point index (D5).  Outputs per bubble: ls, ss, rep (nb*d), info (nb*3: extent, nnDist, n).
+ * Empty bubbles: all zero. */
+int hdb_bubble_stats(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const int32_t *bubble_of, int64_t nb,
+                     int32_t variant, double *ls, double *ss, double *rep, double *info);
+
+/* ------------------------------------------------------------- bubble model (a13-a15)
+ * HdbscanDataBubbles.calculateCoreDistancesBubbles(double[][] repB, int[] nB, double[] eB,
+ * double[] nnDistB, int k, DistanceCalculator) (HdbscanDataBubbles.java:75-76). */
+int hdb_bubble_core_distances(hdb_ctx *ctx, const double *rep, const int32_t *nB, const double *eB,
+                              const double *nnB, int64_t b, int32_t d, int32_t min_pts, int32_t metric,
+                              double *core_out);
+
+/* HdbscanDataBubbles.constructMSTBubbles(...) (HdbscanDataBubbles.java:165-167). */
+int hdb_bubble_prim_mst(hdb_ctx *ctx, const double *rep, const double *eB, const double *nnB,
+                        const int32_t *id_bubbles, const double *core, int64_t b, int32_t d, int32_t metric,
+                        int32_t self_edges, int32_t *va, int32_t *vb, double *w);
+
+/* LocalModelReduceByKey.call body (LocalModelReduceByKey.java:88-104) with D4 vertex ids
+ * 0..b-1: bubble cores, bubble Prim, UndirectedGraph.quicksortByEdgeWeight, cluster tree,
+ * FOSC + noise reassignment, inter-cluster edges.  info = b*3 (extent, nnDist, n).
+ * Outputs: labels[b]; mst_* (2b-1, quicksorted ascending, nullable); ic_* (capacity 2b-1),
+ * *n_ic = number of inter-cluster edges.  Host memory only for outputs. */
+int hdb_local_model(hdb_ctx *ctx, const double *rep, const double *info, int64_t b, int32_t d, int32_t min_pts,
+                    int32_t min_cl_size, int32_t metric, int32_t *labels, int32_t *mst_va, int32_t *mst_vb,
+                    double *mst_w, int32_t *ic_va, int32_t *ic_vb, double *ic_w, int64_t *n_ic);
+
+/* UndirectedGraph.quicksortByEdgeWeight (UndirectedGraph.java:93-124), in place, host. */
+int hdb_quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne);
+
+/* ------------------------------------------------------------------- merge (a20)
+ * UnionFindReducer.call + SortMST (UnionFindReducer.java:19-69, SortMST.java:9-17): stable
+ * sort by DESCENDING weight of the concatenated local edge lists, in place (device radix
+ * sort).  The cross-GPU all-gather feeding it runs over RCCL in the host layer. */
+int hdb_sort_edges_desc(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HDBMI_H */

@@ -1,0 +1,361 @@
+"""Parity of the HIP path (through the C-ABI) against the CPU oracle and the committed
+golden fixtures.  Bar: bit-exact for every value the reference computes in double
+arithmetic with +,-,*,/,sqrt (core distances, MST weights, distances, bubble LS/SS/rep/
+extent) and for every integer/index output (edges, nearest sample, labels); 1e-9 relative
+for the CF variant's real-exponent Math.pow (ClusterFeatureDataBubbles.java:213).
+"""
+import numpy as np
+import pytest
+
+from conftest import blobs, golden, load_iris, load_skin
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def star(pkg):
+    return pkg.HDBSCANStar()
+
+
+def eq(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint8) if a.dtype == np.float64 else a,
+                                                 b.view(np.uint8) if b.dtype == np.float64 else b)
+
+
+# ------------------------------------------------------------------ distance
+def test_distance_rows_bitexact_incl_sqrt_rounding(pkg, oracle):
+    rng = np.random.default_rng(0)
+    for d in (1, 2, 3, 8, 16):
+        a = rng.normal(size=(20000, d)) * rng.choice([1e-3, 1, 1e3, 1e150], size=(20000, 1))
+        b = a + rng.normal(size=(20000, d)) * 1e-2
+        for name in ["euclidean", "cosine", "pearson", "manhattan", "supremum"]:
+            got = pkg.distance_rows(a, b, name)
+            ref = np.array([oracle.distance(a[i], b[i], name) for i in range(0, 20000, 97)])
+            assert eq(got[::97], ref), (d, name)
+
+
+# ------------------------------------------------------------ core distances
+@pytest.mark.parametrize("name", ["iris", "skin3k", "blobs2k"])
+def test_core_distances_golden(star, name):
+    g = golden(name)
+    for sem, tag in [(0, "cum"), (1, "incl"), (2, "excl")]:
+        assert eq(star.calculateCoreDistances(g["X"], 4, None, sem), g[f"core_{tag}"]), tag
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 4, 5, 6, 7, 8, 16])
+@pytest.mark.parametrize("min_pts", [1, 2, 4, 8, 16, 32])
+def test_core_distances_vs_oracle(star, oracle, d, min_pts):
+    X = blobs(1500, d, 5, d * 100 + min_pts)
+    for sem in range(3):
+        assert eq(star.calculateCoreDistances(X, min_pts, None, sem), oracle.core_distances(X, min_pts, semantics=sem))
+
+
+def test_core_distances_ragged_and_tiny(star, oracle):
+    for n in (1, 2, 3, 5, 255, 257, 1023, 1025):
+        X = blobs(n, 3, 2, n)
+        for sem in range(3):
+            assert eq(star.calculateCoreDistances(X, 4, None, sem), oracle.core_distances(X, 4, semantics=sem)), n
+
+
+def test_core_distances_duplicates_skin(star, oracle):
+    X = load_skin(6000)  # integer RGB with heavy duplication: exact zero distances
+    for sem in range(3):
+        assert eq(star.calculateCoreDistances(X, 4, None, sem), oracle.core_distances(X, 4, semantics=sem))
+
+
+def test_core_distances_other_metrics(star):
+    g = golden("metrics300")
+    for name in ["euclidean", "cosine", "pearson", "manhattan", "supremum"]:
+        for tag, sem in [("incl", 1), ("excl", 2), ("cum", 0)]:
+            assert eq(star.calculateCoreDistances(g["X"], 5, name, sem), g[f"{name}_core_{tag}"]), (name, tag)
+
+
+def test_knn_lists_and_indices(star, oracle):
+    X = blobs(3000, 3, 4, 9)
+    for k in (1, 3, 7, 15):
+        ref = oracle.knn_lists(X, k + 1, excl_self=True)
+        dist, idx = star.knn(X, k, None, exclSelf=True, withIndices=True)
+        assert eq(dist, ref)
+        # indices point at a row with exactly that distance
+        for r in range(0, 3000, 137):
+            for c in range(k):
+                j = idx[r, c]
+                assert j != r and oracle.distance(X[r], X[j]) == dist[r, c]
+
+
+def test_core_distances_device_tensors(star, oracle):
+    import torch
+    X = blobs(5000, 3, 6, 1)
+    t = torch.from_numpy(X).cuda()
+    got = star.calculateCoreDistances(t, 4, None, 2)
+    assert got.is_cuda
+    assert eq(got.cpu().numpy(), oracle.core_distances(X, 4, semantics=2))
+
+
+def test_core_distances_full_size_rows(star):
+    """BASELINE config 2 size (1M x 3): exact per-row check on a row sample -- numpy
+    elementwise ops follow the Java order (no FMA), sqrt is correctly rounded."""
+    import torch
+    X = blobs(1_000_000, 3, 20, 1)
+    got = star.calculateCoreDistances(torch.from_numpy(X).cuda(), 4, None, 2).cpu().numpy()
+    rng = np.random.default_rng(5)
+    for r in rng.choice(X.shape[0], 24, replace=False):
+        s = (X[r, 0] - X[:, 0]) * (X[r, 0] - X[:, 0])
+        s = s + (X[r, 1] - X[:, 1]) * (X[r, 1] - X[:, 1])
+        s = s + (X[r, 2] - X[:, 2]) * (X[r, 2] - X[:, 2])
+        s[r] = np.inf
+        ref = np.sqrt(np.partition(s, 2)[:3].max())
+        assert got[r] == ref, r
+
+
+# ----------------------------------------------------------------------- MST
+@pytest.mark.parametrize("name", ["iris", "skin3k", "blobs2k"])
+def test_prim_golden(star, name):
+    g = golden(name)
+    for tag in ["cum", "incl", "excl"]:
+        mst = star.constructMST(g["X"], g[f"core_{tag}"], True, None, g["ids"])
+        assert eq(mst.getVerticeA(), g[f"prim_{tag}_va"]), tag
+        assert eq(mst.getVericeB(), g[f"prim_{tag}_vb"]), tag
+        assert eq(mst.getEges(), g[f"prim_{tag}_w"]), tag
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 63, 64, 65, 256, 257, 1024, 1025, 4096, 4097, 7000])
+def test_prim_sizes_vs_oracle(star, oracle, n):
+    X = np.round(blobs(n, 3, 4, n), 2)  # rounding -> many exact MRD ties
+    core = oracle.core_distances(X, 4, semantics=2)
+    ids = np.arange(n, dtype=np.int32) * 3 + 1
+    mst = star.constructMST(X, core, True, None, ids)
+    va, vb, w = oracle.prim_mst(X, core, ids)
+    assert eq(mst.getVerticeA(), va) and eq(mst.getVericeB(), vb) and eq(mst.getEges(), w)
+
+
+def test_prim_other_metrics_golden(star):
+    g = golden("metrics300")
+    for name in ["euclidean", "cosine", "pearson", "manhattan", "supremum"]:
+        mst = star.constructMST(g["X"], g[f"{name}_core_incl"], True, name)
+        assert eq(mst.getVerticeA(), g[f"{name}_va"]) and eq(mst.getEges(), g[f"{name}_w"]), name
+
+
+def test_prim_batched_partitions(pkg, oracle):
+    import ctypes as C
+    sizes = [1, 5, 50, 64, 300, 1000, 4100, 2]
+    X = np.round(blobs(sum(sizes), 3, 4, 77), 2)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    core = oracle.core_distances(X, 4, semantics=2)  # any cores
+    ids = np.arange(X.shape[0], dtype=np.int32) + 100
+    ne = sum(2 * s - 1 for s in sizes)
+    va, vb, w = np.zeros(ne, np.int32), np.zeros(ne, np.int32), np.zeros(ne)
+    ctx = pkg.Context.get(0)
+    A = pkg._capi
+    A.check(A.lib().hdb_prim_mst_batched(ctx.h, A.ptr(X), A.ptr(off), len(sizes), 3, A.ptr(core), A.ptr(ids), 0, 1,
+                                         A.ptr(va), A.ptr(vb), A.ptr(w)), "batched")
+    e = 0
+    for p, s in enumerate(sizes):
+        ra, rb, rw = oracle.prim_mst(X[off[p]:off[p + 1]], core[off[p]:off[p + 1]], ids[off[p]:off[p + 1]])
+        assert eq(va[e:e + 2 * s - 1], ra) and eq(vb[e:e + 2 * s - 1], rb) and eq(w[e:e + 2 * s - 1], rw), p
+        e += 2 * s - 1
+
+
+def test_first_step_leaf_batched(pkg, oracle):
+    """FirstStep leaf branch (FirstStep.java:104-120) for many partitions at once."""
+    sizes = [50, 49, 1, 2, 37, 50, 3, 4100]
+    X = load_skin(sum(sizes))
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    ids = np.arange(X.shape[0], dtype=np.int32) + 5
+    fs = pkg.FirstStep(0.2, 50, 4)
+    core, mst = fs.leaf(X, ids, off)
+    e = 0
+    for p, s in enumerate(sizes):
+        rc, (ra, rb, rw) = oracle.first_step_leaf(X[off[p]:off[p + 1]], ids[off[p]:off[p + 1]], 4)
+        assert eq(core[off[p]:off[p + 1]], rc), p
+        sl = slice(e, e + 2 * s - 1)
+        assert eq(mst.getVerticeA()[sl], ra) and eq(mst.getVericeB()[sl], rb) and eq(mst.getEges()[sl], rw), p
+        e += 2 * s - 1
+
+
+def _check_spanning_tree(n, va, vb):
+    parent = list(range(n))
+
+    def find(x):
+        while parent[x] != x:
+            parent[x] = parent[parent[x]]
+            x = parent[x]
+        return x
+    for a, b in zip(va, vb):
+        ra, rb = find(int(a)), find(int(b))
+        assert ra != rb, "cycle"
+        parent[ra] = rb
+    assert len({find(i) for i in range(n)}) == 1
+
+
+@pytest.mark.parametrize("n,d", [(2, 3), (100, 3), (5000, 3), (6000, 2), (3000, 8), (20000, 3)])
+def test_boruvka_weights_equal_prim(star, oracle, n, d):
+    X = np.round(blobs(n, d, 6, n + d), 1)  # heavy ties
+    core = oracle.core_distances(X, 4, semantics=2)
+    mst = star.constructMSTBoruvka(X, core, False)
+    _, _, w = oracle.prim_mst(X, core, self_edges=False)
+    assert eq(np.sort(mst.getEges()), np.sort(w))  # MST weight multiset is unique
+    _check_spanning_tree(n, mst.getVerticeA(), mst.getVericeB())
+    # edges are reported sorted by (w, lo, hi)
+    k = np.lexsort((mst.getVericeB(), mst.getVerticeA(), mst.getEges()))
+    assert np.array_equal(k, np.arange(n - 1))
+
+
+def test_boruvka_large_vs_gpu_prim(star):
+    """Borůvka vs the (exact) stepwise GPU Prim on a 60k graph: identical sorted weights."""
+    import torch
+    X = blobs(60000, 3, 20, 1)
+    t = torch.from_numpy(X).cuda()
+    core = star.calculateCoreDistances(t, 4, None, 2)
+    wb = star.constructMSTBoruvka(t, core, False).getEges().cpu().numpy()
+    wp = star.constructMST(t, core, False).getEges().cpu().numpy()
+    assert eq(np.sort(wb), np.sort(wp))
+
+
+# ------------------------------------------------------------ nearest sample
+@pytest.mark.parametrize("name", ["iris", "skin3k"])
+def test_nearest_golden(pkg, name):
+    g = golden(name)
+    idx, dist = pkg.nearest_sample(g["X"], g["ns_S"], with_dist=True)
+    assert eq(idx, g["ns_idx"]) and eq(dist, g["ns_dist"])
+
+
+def test_nearest_other_metrics(pkg):
+    g = golden("metrics300")
+    for name in ["euclidean", "cosine", "pearson", "manhattan", "supremum"]:
+        idx, dist = pkg.nearest_sample(g["X"], g["S"], name, with_dist=True)
+        assert eq(idx, g[f"{name}_ns_idx"]) and eq(dist, g[f"{name}_ns_dist"]), name
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 4, 5, 6, 7, 8, 16])
+def test_nearest_vs_oracle(pkg, oracle, d):
+    X = np.round(blobs(4000, d, 5, d), 1)
+    S = X[::7].copy()
+    idx, dist = pkg.nearest_sample(X, S, with_dist=True)
+    r_idx, r_dist = oracle.nearest_sample(X, S)
+    assert eq(idx, r_idx) and eq(dist, r_dist)
+
+
+def test_nearest_keyed(pkg, oracle):
+    rng = np.random.default_rng(4)
+    X = np.round(blobs(5000, 3, 5, 4), 1)
+    xk = rng.integers(0, 7, 5000).astype(np.int32)
+    S = X[::9].copy()
+    sk = xk[::9].copy()
+    sk[sk == 6] = 5  # key 6 has no samples -> index 0 / MAX as the Java init
+    idx, dist = pkg.nearest_sample(X, S, None, xk, sk, with_dist=True)
+    r_idx, r_dist = oracle.nearest_sample(X, S, x_key=xk, s_key=sk)
+    assert eq(idx, r_idx) and eq(dist, r_dist)
+
+
+def test_nearest_sqrt_ties(pkg, oracle):
+    """Two samples whose squared distances differ but whose sqrt values are equal: Java's
+    strict '<' on sqrt values keeps the FIRST; an argmin on squares would pick the second."""
+    rng = np.random.default_rng(11)
+    c = rng.normal(size=(400000, 2))
+    c /= np.sqrt((c * c).sum(1))[:, None]
+    s = c[:, 0] * c[:, 0] + c[:, 1] * c[:, 1]
+    r = np.sqrt(s)
+    order = np.lexsort((s, r))
+    found = None
+    for a, b in zip(order[:-1], order[1:]):
+        if r[a] == r[b] and s[a] < s[b]:
+            found = (b, a)  # larger square first
+            break
+    assert found is not None
+    S = np.stack([c[found[0]], c[found[1]], [5.0, 5.0]])
+    X = np.zeros((3, 2))
+    idx, dist = pkg.nearest_sample(X, S, with_dist=True)
+    r_idx, r_dist = oracle.nearest_sample(X, S)
+    assert eq(idx, r_idx) and idx[0] == 0 and eq(dist, r_dist)
+
+
+# ------------------------------------------------------------- bubble stats
+@pytest.mark.parametrize("name", ["iris", "skin_bubbles2k", "blobs2k"])
+def test_bubble_stats_golden(pkg, name):
+    g = golden(name)
+    ls, ss, rep, info = pkg.bubble_stats(g["X"], g["b_bubble_of"], g["b_used"].shape[0])
+    assert eq(ls, g["b_ls"]) and eq(ss, g["b_ss"]) and eq(rep, g["b_rep"]) and eq(info, g["b_info"])
+
+
+def test_bubble_stats_cf(pkg):
+    g = golden("blobs2k")
+    ls, ss, rep, info = pkg.bubble_stats(g["X"], g["b_bubble_of"], g["b_used"].shape[0], pkg.BUBBLE_CF)
+    assert eq(rep, g["cf_rep"]) and eq(ls, g["cf_ls"]) and eq(info[:, 0], g["cf_info"][:, 0])
+    np.testing.assert_allclose(info[:, 1], g["cf_info"][:, 1], rtol=1e-9)  # real-exponent pow
+
+
+def test_bubble_stats_empty_and_d1(pkg, oracle):
+    X = np.random.default_rng(1).normal(size=(1000, 1))
+    bo = np.random.default_rng(2).integers(0, 300, 1000).astype(np.int32)
+    bo[bo == 7] = 8  # bubble 7 empty
+    ls, ss, rep, info = pkg.bubble_stats(X, bo, 300)
+    r = oracle.bubble_stats(X, bo, 300)
+    assert eq(ls, r["ls"]) and eq(ss, r["ss"]) and eq(rep, r["rep"]) and eq(info, r["info"])
+
+
+# -------------------------------------------------------------- bubble model
+@pytest.mark.parametrize("name", ["iris", "skin_bubbles2k", "blobs2k"])
+def test_bubble_core_and_prim_vs_oracle(pkg, oracle, name):
+    g = golden(name)
+    rep, info = g["b_rep"], g["b_info"]
+    nB, eB, nnB = info[:, 2].astype(np.int32), info[:, 0].copy(), info[:, 1].copy()
+    model = pkg.HdbscanDataBubbles()
+    core = model.calculateCoreDistancesBubbles(rep, nB, eB, nnB, 4)
+    assert eq(core, oracle.bubble_core_distances(rep, nB, eB, nnB, 4))
+    ids = np.arange(rep.shape[0], dtype=np.int32)
+    mst = model.constructMSTBubbles(rep, nB, eB, nnB, ids, core, True)
+    va, vb, w = oracle.bubble_prim_mst(rep, eB, nnB, core, ids)
+    assert eq(mst.getVerticeA(), va) and eq(mst.getEges(), w)
+
+
+@pytest.mark.parametrize("name", ["iris", "skin_bubbles2k", "blobs2k"])
+def test_local_model_golden(pkg, name):
+    g = golden(name)
+    op = pkg.LocalModelReduceByKey(4, 4)
+    labels, mst, (iva, ivb, iw) = op.call(g["b_rep"], g["b_info"])
+    assert eq(labels, g["b_labels"])
+    assert eq(mst.getVerticeA(), g["b_mst_va"]) and eq(mst.getEges(), g["b_mst_w"])
+    assert eq(iva, g["b_ic_va"]) and eq(ivb, g["b_ic_vb"]) and eq(iw, g["b_ic_w"])
+
+
+def test_local_model_larger_vs_oracle(pkg, oracle):
+    """A 5k-bubble model: stepwise bubble Prim path (b > 4096)."""
+    X = blobs(30000, 3, 8, 12)
+    rng = np.random.default_rng(12)
+    sids = np.sort(rng.choice(30000, 5000, replace=False))
+    near, _ = oracle.nearest_sample(X, X[sids])
+    used = np.unique(near)
+    remap = -np.ones(5000, np.int32)
+    remap[used] = np.arange(used.shape[0], dtype=np.int32)
+    st = oracle.bubble_stats(X, remap[near], used.shape[0])
+    lm = oracle.local_model(st["rep"], st["info"], 4, 4)
+    labels, mst, inter = pkg.LocalModelReduceByKey(4, 4).call(st["rep"], st["info"])
+    assert eq(labels, lm["labels"]) and eq(mst.getEges(), lm["mst"][2]) and eq(inter[2], lm["inter"][2])
+
+
+# --------------------------------------------------------------------- merge
+def test_sort_edges_desc_golden(pkg):
+    g = golden("merge")
+    va, vb, w = pkg.sort_edges_desc(g["in_va"].copy(), g["in_vb"].copy(), g["in_w"].copy())
+    assert eq(va, g["va"]) and eq(vb, g["vb"]) and eq(w, g["w"])
+
+
+def test_sort_edges_desc_large_stable(pkg, oracle):
+    rng = np.random.default_rng(8)
+    n = 300000
+    w = np.round(rng.uniform(0, 50, n), 2)
+    a = rng.integers(0, 1 << 30, n).astype(np.int32)
+    b = rng.integers(0, 1 << 30, n).astype(np.int32)
+    ga, gb, gw = pkg.sort_edges_desc(a.copy(), b.copy(), w.copy())
+    ra, rb, rw = oracle.merge_edges([(a, b, w)])
+    assert eq(ga, ra) and eq(gb, rb) and eq(gw, rw)
+
+
+# -------------------------------------------------------------------- errors
+def test_errors_map_to_reference_exceptions(pkg, star):
+    with pytest.raises(pkg.HdbError):
+        star.calculateCoreDistances(np.zeros((10, 3)), 0)  # minPts < 1
+    with pytest.raises(pkg.HdbError):
+        star.calculateCoreDistances(np.zeros((10, 3)), 40)  # > 32 unsupported
