@@ -63,6 +63,14 @@ def lib():
     with _lock:
         if _lib is not None:
             return _lib
+        # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 (SONAME
+        # libamdhip64.so.7).  Loading torch first lets this library's NEEDED entry bind to
+        # that runtime, so device pointers of torch tensors are valid here.  Loading us
+        # first would map /opt/rocm's runtime and torch would then map a second one.
+        try:
+            import torch  # noqa: F401
+        except ImportError:  # pragma: no cover - standalone use: /opt/rocm runtime
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"libhdbmi.so not built ({LIB_PATH}); run build_lib.py / __graft_entry__.build()")
         L = C.CDLL(LIB_PATH)

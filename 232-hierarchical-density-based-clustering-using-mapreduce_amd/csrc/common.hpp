@@ -48,6 +48,8 @@ struct hdb_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    hipStream_t side = nullptr;  // private non-blocking stream for graph capture (the null
+                                 // stream cannot be captured); fenced to `stream` by events
     bool timing = false;
     std::vector<hdb::TimedLaunch> pending;
     std::vector<hipEvent_t> event_pool;
@@ -62,6 +64,8 @@ namespace hdb {
 enum { A_STAGE_IN = 0, A_STAGE_OUT = 1, A_WORK0 = 2, A_WORK1 = 3, A_WORK2 = 4, A_WORK3 = 5, A_PAD = 6, A_SORT = 7 };
 
 void *arena(hdb_ctx *ctx, int slot, size_t bytes);
+// order `to` after all work queued so far on `from` (event record + stream wait)
+void stream_fence(hdb_ctx *ctx, hipStream_t from, hipStream_t to);
 
 // kernel timing helpers: begin/end around a launch of a named kernel
 void time_begin(hdb_ctx *ctx, const char *name, TimedLaunch &t);

@@ -35,6 +35,14 @@ static hipEvent_t get_event(hdb_ctx *ctx) {
     return e;
 }
 
+void stream_fence(hdb_ctx *ctx, hipStream_t from, hipStream_t to) {
+    if (from == to) return;
+    hipEvent_t e = get_event(ctx);
+    HIP_CHECK(hipEventRecord(e, from));
+    HIP_CHECK(hipStreamWaitEvent(to, e, 0));
+    ctx->event_pool.push_back(e);  // reusable: re-recording only affects later waits
+}
+
 void time_begin(hdb_ctx *ctx, const char *name, TimedLaunch &t) {
     t.name = name;
     t.a = get_event(ctx);
@@ -127,6 +135,7 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         c->device = device;
         HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         c->own_stream = true;
+        HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         hipDeviceProp_t prop;
         HIP_CHECK(hipGetDeviceProperties(&prop, device));
         c->num_cus = prop.multiProcessorCount;
@@ -150,6 +159,10 @@ void hdb_ctx_destroy(hdb_ctx *ctx) {
     for (auto &a : ctx->arenas)
         if (a.ptr) (void)hipFree(a.ptr);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->side) {
+        (void)hipStreamSynchronize(ctx->side);
+        (void)hipStreamDestroy(ctx->side);
+    }
     delete ctx;
 }
 
@@ -159,13 +172,11 @@ int hdb_ctx_set_stream(hdb_ctx *ctx, void *stream) {
         HIP_CHECK(hipSetDevice(ctx->device));
         HIP_CHECK(hipStreamSynchronize(ctx->stream));
         if (ctx->own_stream) HIP_CHECK(hipStreamDestroy(ctx->stream));
-        if (stream) {
-            ctx->stream = (hipStream_t)stream;
-            ctx->own_stream = false;
-        } else {
-            HIP_CHECK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-            ctx->own_stream = true;
-        }
+        // NULL selects the device's default (null) stream -- what PyTorch reports as
+        // current_stream().cuda_stream == 0 -- never a private stream, so work stays
+        // ordered with the caller's.
+        ctx->stream = (hipStream_t)stream;
+        ctx->own_stream = false;
         return HDB_OK;
     } catch (const Error &e) {
         set_error(e.msg);

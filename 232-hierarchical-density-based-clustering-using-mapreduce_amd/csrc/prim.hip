@@ -435,46 +435,60 @@ void prim_batched_device(hdb_ctx *ctx, const PrimIn &in, const int64_t *h_offs, 
                            st.att, total_v);
         int64_t maxn = 0;
         for (int32_t p : cls[4]) maxn = std::max(maxn, h_offs[p + 1] - h_offs[p]);
-        // steps 1..maxn-1; chunks captured into a hipGraph and replayed
+        // steps 1..maxn-1 run on the context's side stream (capturable) in chunks captured
+        // into a hipGraph and replayed; fenced to/from the caller's stream by events.
         const int CH = 256;
+        hipStream_t ss = ctx->side;
+        stream_fence(ctx, ctx->stream, ss);
         hipGraphExec_t exec = nullptr;
         KernelTimer t(ctx, "prim_step_total");
         int step = 1;
-        // eager for the first partial chunk so the graph chunk starts at an odd step
         auto launch_one = [&](int s) {
-            hipLaunchKernelGGL((prim_step_kernel<SBS, SPPT>), dim3(nwg), dim3(SBS), 0, ctx->stream, in, d_off, d_wgp,
-                               d_wgf, d_wgc, st, s, s & 1);
+            hipLaunchKernelGGL((prim_step_kernel<SBS, SPPT>), dim3(nwg), dim3(SBS), 0, ss, in, d_off, d_wgp, d_wgf,
+                               d_wgc, st, s, s & 1);
         };
-        while (step < maxn) {
-            int remain = (int)(maxn - step);
-            if (remain < CH || ctx->timing) {
-                for (int s = 0; s < std::min(remain, CH); s++) launch_one(step + s);
-                HIP_CHECK(hipGetLastError());
-                step += std::min(remain, CH);
-                continue;
-            }
-            // capture CH launches with absolute steps; re-capture per chunk (steps are args)
-            hipGraph_t graph;
-            HIP_CHECK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-            for (int s = 0; s < CH; s++) launch_one(step + s);
-            HIP_CHECK(hipStreamEndCapture(ctx->stream, &graph));
-            if (!exec) {
-                HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-            } else {
-                hipGraphExecUpdateResult res;
-                hipGraphNode_t errn;
-                if (hipGraphExecUpdate(exec, graph, &errn, &res) != hipSuccess) {
-                    (void)hipGetLastError();
-                    HIP_CHECK(hipGraphExecDestroy(exec));
-                    HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+        try {
+            while (step < maxn) {
+                int remain = (int)(maxn - step);
+                if (remain < CH) {
+                    for (int s = 0; s < remain; s++) launch_one(step + s);
+                    HIP_CHECK(hipGetLastError());
+                    step += remain;
+                    continue;
                 }
+                hipGraph_t graph;
+                HIP_CHECK(hipStreamBeginCapture(ss, hipStreamCaptureModeThreadLocal));
+                for (int s = 0; s < CH; s++) launch_one(step + s);
+                hipError_t ce = hipStreamEndCapture(ss, &graph);
+                HIP_CHECK(ce);
+                if (!exec) {
+                    HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+                } else {
+                    hipGraphExecUpdateResult res;
+                    hipGraphNode_t errn;
+                    if (hipGraphExecUpdate(exec, graph, &errn, &res) != hipSuccess) {
+                        (void)hipGetLastError();
+                        HIP_CHECK(hipGraphExecDestroy(exec));
+                        HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+                    }
+                }
+                HIP_CHECK(hipGraphLaunch(exec, ss));
+                HIP_CHECK(hipGraphDestroy(graph));
+                step += CH;
             }
-            HIP_CHECK(hipGraphLaunch(exec, ctx->stream));
-            HIP_CHECK(hipGraphDestroy(graph));
-            step += CH;
+        } catch (...) {
+            hipGraph_t g = nullptr;
+            hipStreamCaptureStatus cs;
+            if (hipStreamIsCapturing(ss, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) {
+                (void)hipStreamEndCapture(ss, &g);
+                if (g) (void)hipGraphDestroy(g);
+            }
+            if (exec) (void)hipGraphExecDestroy(exec);
+            throw;
         }
+        stream_fence(ctx, ss, ctx->stream);
         if (exec) {
-            HIP_CHECK(hipStreamSynchronize(ctx->stream));
+            HIP_CHECK(hipStreamSynchronize(ss));
             HIP_CHECK(hipGraphExecDestroy(exec));
         }
         // edges for stepwise partitions

@@ -57,7 +57,8 @@ typedef struct hdb_ctx hdb_ctx;
 /* ------------------------------------------------------------------ context */
 int hdb_ctx_create(int device, hdb_ctx **out);
 void hdb_ctx_destroy(hdb_ctx *ctx);
-/* Run on a caller-owned hipStream_t (e.g. torch's current stream); NULL = context-owned. */
+/* Run on a caller-owned hipStream_t (e.g. torch's current stream); NULL = the device's default
+ * (null) stream.  A fresh context owns a private non-blocking stream until this is called. */
 int hdb_ctx_set_stream(hdb_ctx *ctx, void *hip_stream);
 /* Per-kernel HIP-event timing (off by default). */
 int hdb_ctx_set_timing(hdb_ctx *ctx, int enable);

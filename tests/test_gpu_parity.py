@@ -18,9 +18,17 @@ def star(pkg):
 
 
 def eq(a, b):
-    a, b = np.asarray(a), np.asarray(b)
-    return a.shape == b.shape and np.array_equal(a.view(np.uint8) if a.dtype == np.float64 else a,
-                                                 b.view(np.uint8) if b.dtype == np.float64 else b)
+    """Bit-exact equality (NaN == NaN regardless of payload, as Java's NaN is one value)."""
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    if a.shape != b.shape:
+        return False
+    if a.dtype == np.float64:
+        na, nb = np.isnan(a), np.isnan(b)
+        if not np.array_equal(na, nb):
+            return False
+        a, b = np.where(na, 0.0, a), np.where(nb, 0.0, b)
+        return np.array_equal(a.view(np.uint64), b.view(np.uint64))
+    return np.array_equal(a, b)
 
 
 # ------------------------------------------------------------------ distance
@@ -320,18 +328,27 @@ def test_local_model_golden(pkg, name):
     assert eq(iva, g["b_ic_va"]) and eq(ivb, g["b_ic_vb"]) and eq(iw, g["b_ic_w"])
 
 
-def test_local_model_larger_vs_oracle(pkg, oracle):
-    """A 5k-bubble model: stepwise bubble Prim path (b > 4096)."""
-    X = blobs(30000, 3, 8, 12)
-    rng = np.random.default_rng(12)
+@pytest.mark.parametrize("seed,min_pts,mcl", [(12, 4, 4), (13, 4, 16), (16, 4, 4), (17, 8, 8)])
+def test_local_model_larger_vs_oracle(pkg, oracle, seed, min_pts, mcl):
+    """~5k-bubble models (stepwise bubble Prim path, b > 4096).  When the reference itself
+    throws (duplicate components -> "Cluster cannot have less than 0 points",
+    Clusters.java:45-46) the product must raise the same exception."""
+    X = blobs(30000, 3, 8, seed)
+    rng = np.random.default_rng(seed)
     sids = np.sort(rng.choice(30000, 5000, replace=False))
     near, _ = oracle.nearest_sample(X, X[sids])
     used = np.unique(near)
     remap = -np.ones(5000, np.int32)
     remap[used] = np.arange(used.shape[0], dtype=np.int32)
     st = oracle.bubble_stats(X, remap[near], used.shape[0])
-    lm = oracle.local_model(st["rep"], st["info"], 4, 4)
-    labels, mst, inter = pkg.LocalModelReduceByKey(4, 4).call(st["rep"], st["info"])
+    try:
+        lm = oracle.local_model(st["rep"], st["info"], min_pts, mcl)
+    except oracle.OracleError as e:
+        assert e.code == -12
+        with pytest.raises(pkg.IllegalStateException):
+            pkg.LocalModelReduceByKey(min_pts, mcl).call(st["rep"], st["info"])
+        return
+    labels, mst, inter = pkg.LocalModelReduceByKey(min_pts, mcl).call(st["rep"], st["info"])
     assert eq(labels, lm["labels"]) and eq(mst.getEges(), lm["mst"][2]) and eq(inter[2], lm["inter"][2])
 
 
