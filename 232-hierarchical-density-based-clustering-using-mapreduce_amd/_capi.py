@@ -82,6 +82,7 @@ def lib():
             "hdb_ctx_set_timing": [vp, C.c_int],
             "hdb_ctx_kernel_time": [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int],
             "hdb_ctx_synchronize": [vp],
+            "hdb_ctx_set_option": [vp, C.c_char_p, C.c_int64],
             "hdb_distance_rows": [vp, dp, dp, i64, i32, i32, dp],
             "hdb_core_distances": [vp, dp, i64, i32, i32, i32, i32, dp],
             "hdb_knn": [vp, dp, i64, i32, i32, i32, i32, dp, ip],
@@ -109,7 +110,7 @@ def lib():
     return _lib
 
 
-EXPORTED = ["hdb_ctx_create", "hdb_ctx_destroy", "hdb_ctx_set_stream", "hdb_ctx_set_timing",
+EXPORTED = ["hdb_ctx_create", "hdb_ctx_destroy", "hdb_ctx_set_stream", "hdb_ctx_set_timing", "hdb_ctx_set_option",
             "hdb_ctx_kernel_time", "hdb_ctx_synchronize", "hdb_last_error", "hdb_version",
             "hdb_distance_rows", "hdb_core_distances", "hdb_knn", "hdb_prim_mst", "hdb_prim_mst_batched",
             "hdb_leaf_msts", "hdb_mst_boruvka", "hdb_nearest_sample", "hdb_bubble_stats",
@@ -163,6 +164,9 @@ class Context:
         check(lib().hdb_ctx_kernel_time(self.h, name.encode(), C.byref(ms), C.byref(n), int(reset)),
               "hdb_ctx_kernel_time")
         return ms.value, n.value
+
+    def set_option(self, name: str, value: int):
+        check(lib().hdb_ctx_set_option(self.h, name.encode(), int(value)), "hdb_ctx_set_option")
 
     def synchronize(self):
         check(lib().hdb_ctx_synchronize(self.h), "hdb_ctx_synchronize")

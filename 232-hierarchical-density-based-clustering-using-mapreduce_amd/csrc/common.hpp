@@ -56,6 +56,7 @@ struct hdb_ctx {
     std::map<std::string, std::pair<double, int64_t>> acc;
     hdb::Arena arenas[8];
     int num_cus = 256;
+    bool force_fp64 = false;  // disable the FP32 screen in K1 (A/B and tests)
 };
 
 namespace hdb {

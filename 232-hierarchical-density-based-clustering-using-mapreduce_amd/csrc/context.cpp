@@ -212,6 +212,16 @@ int hdb_ctx_kernel_time(hdb_ctx *ctx, const char *name, double *ms_total, int64_
     }
 }
 
+int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
+    if (!ctx || !name) return HDB_EINVAL;
+    if (std::string(name) == "knn_fp32_screen") {
+        ctx->force_fp64 = value == 0;
+        return HDB_OK;
+    }
+    set_error(std::string("unknown option ") + name);
+    return HDB_EINVAL;
+}
+
 int hdb_ctx_synchronize(hdb_ctx *ctx) {
     try {
         if (!ctx) HDB_THROW(HDB_EINVAL, "ctx is NULL");

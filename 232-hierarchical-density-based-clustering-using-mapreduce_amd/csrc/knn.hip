@@ -171,6 +171,198 @@ __global__ __launch_bounds__(256) void knn_sq_kernel(const double *__restrict__ 
     }
 }
 
+// ----------------------------------------------- FP32-filtered exact kernel
+// Same contract as knn_sq_kernel, but each pair is first screened in FP32 (2-cycle VALU
+// ops instead of 4-cycle FP64): coordinates are shifted by the data's bounding-box centre
+// and rounded to FP32 (Xf), s32 = sum (xf - cf)^2 with fmaf.  A rigorous bound makes the
+// screen conservative: with M' = max |x - centre| and E = sqrt(d) * 4 * 2^-24 * M' * 1.01,
+//   ||x - c|| >= sqrt(s32 / (1 + d 2^-24)) - E,
+// so s32 >= thr(tau) = ((sqrt(tau (1+1e-14)) + E)^2 (1 + 1e-5)) rounded up to FP32 proves
+// the exact FP64 s64 >= tau (no insertion).  A group of U x Q pairs goes to the exact FP64
+// path (the reference's operation order, identical to knn_sq_kernel) only when some lane
+// has a pair below its threshold -- rare once the top-K has warmed up.  Results are the
+// FP64 results bit for bit; the filter only skips provably rejected pairs.
+__device__ __forceinline__ float knn_thr32(double tau, double E) {
+    if (!(tau < INFINITY)) return INFINITY;
+    double r = sqrt(tau * (1.0 + 1e-14)) + E;
+    double T = (r * r) * (1.0 + 1e-5);
+    float f = (float)T;
+    if ((double)f < T) f = nextafterf(f, INFINITY);
+    return f;
+}
+
+template <int D, int DF, int DP, int K, int Q, int U, bool EXCL, bool IDX>
+__global__ __launch_bounds__(256) void knn_f32x_kernel(const float *__restrict__ Xf, const double *__restrict__ Xp,
+                                                       const double *__restrict__ params, int64_t n,
+                                                       int64_t cand_chunk, double *__restrict__ part_v,
+                                                       int32_t *__restrict__ part_i, int finalize) {
+    const int64_t q0 = (int64_t)blockIdx.x * (256 * Q);
+    const int64_t qhi = min(q0 + (int64_t)256 * Q, n);
+    const int64_t c_lo = (int64_t)blockIdx.y * cand_chunk;
+    const int64_t c_hi = min(c_lo + cand_chunk, n);
+    const double E = params[0];
+
+    float xf[Q][D];
+    double xq[Q][D];
+    double buf[Q][K];
+    int bidx[Q][K];
+    float thr[Q];
+    int64_t qi[Q];
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+        qi[q] = q0 + threadIdx.x + (int64_t)q * 256;
+        const int64_t r = qi[q] < n ? qi[q] : 0;
+#pragma unroll
+        for (int c = 0; c < D; c++) {
+            xq[q][c] = Xp[r * DP + c];
+            xf[q][c] = Xf[r * DF + c];
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            buf[q][k] = INFINITY;
+            bidx[q][k] = -1;
+        }
+        thr[q] = INFINITY;
+    }
+    int64_t a = c_hi, b = c_hi;
+    if (EXCL) {
+        a = max(c_lo, min(c_hi, q0));
+        b = max(a, min(c_hi, qhi));
+    }
+#pragma unroll 1
+    for (int seg = 0; seg < 3; seg++) {
+        int64_t s_lo = seg == 0 ? c_lo : (seg == 1 ? a : b);
+        int64_t s_hi = seg == 0 ? a : (seg == 1 ? b : c_hi);
+        const bool chk = EXCL && seg == 1;
+        int64_t j = s_lo;
+#pragma unroll 1
+        for (; j < s_hi; j += U) {
+            const int64_t ucount = min((int64_t)U, s_hi - j);
+            // FP32 screen
+            bool hit = false;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int64_t jj = j + u < s_hi ? j + u : j;  // clamp (masked below)
+                const float *cr = Xf + jj * DF;
+                float cf[D];
+#pragma unroll
+                for (int c = 0; c < D; c++) cf[c] = cr[c];
+#pragma unroll
+                for (int q = 0; q < Q; q++) {
+                    float t0 = xf[q][0] - cf[0];
+                    float acc = t0 * t0;
+#pragma unroll
+                    for (int c = 1; c < D; c++) {
+                        float t = xf[q][c] - cf[c];
+                        acc = __builtin_fmaf(t, t, acc);
+                    }
+                    bool ok = u < ucount && !(acc >= thr[q]);
+                    if (chk && qi[q] == jj) ok = false;
+                    hit |= ok;
+                }
+            }
+            if (!hit) continue;
+            // exact FP64 path for the group (reference operation order)
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (u >= ucount) break;
+                const double *cr = Xp + (j + u) * DP;
+                double cc[D];
+#pragma unroll
+                for (int c = 0; c < D; c++) cc[c] = cr[c];
+#pragma unroll
+                for (int q = 0; q < Q; q++) {
+                    double acc = sq_diff(xq[q][0], cc[0]);
+#pragma unroll
+                    for (int c = 1; c < D; c++) acc = acc + sq_diff(xq[q][c], cc[c]);
+                    if (chk && qi[q] == j + u) acc = INFINITY;
+                    if (acc < buf[q][K - 1]) {
+                        if (IDX) topk_insert_idx<K>(buf[q], bidx[q], acc, (int)(j + u));
+                        else topk_insert<K>(buf[q], acc);
+                        thr[q] = knn_thr32(buf[q][K - 1], E);
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+        if (qi[q] >= n) continue;
+        const int64_t o = ((int64_t)blockIdx.y * n + qi[q]) * K;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            double v = buf[q][k];
+            if (finalize) v = (v < INFINITY) ? sqrt(v) : JMAX;
+            part_v[o + k] = v;
+            if (IDX) part_i[o + k] = (finalize && !(buf[q][k] < INFINITY)) ? -1 : bidx[q][k];
+        }
+    }
+}
+
+// bounding box per dimension (one block per dimension)
+__global__ void knn_bbox_kernel(const double *__restrict__ X, int64_t n, int d, double *__restrict__ lo,
+                                double *__restrict__ hi) {
+    const int c = blockIdx.x;
+    __shared__ double sl[256], sh[256];
+    double l = INFINITY, h = -INFINITY;
+    for (int64_t i = threadIdx.x; i < n; i += 256) {
+        double v = X[i * d + c];
+        l = v < l ? v : l;
+        h = v > h ? v : h;
+        if (v != v) {  // NaN poisons the box -> FP64-only path
+            l = NAN;
+            h = NAN;
+        }
+    }
+    sl[threadIdx.x] = l;
+    sh[threadIdx.x] = h;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            double a = sl[threadIdx.x], b = sl[threadIdx.x + s];
+            sl[threadIdx.x] = (a != a || b != b) ? NAN : (a < b ? a : b);
+            a = sh[threadIdx.x];
+            b = sh[threadIdx.x + s];
+            sh[threadIdx.x] = (a != a || b != b) ? NAN : (a > b ? a : b);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        lo[c] = sl[0];
+        hi[c] = sh[0];
+    }
+}
+
+// shift + FP32 pack; params[0] = E, params[1] = 1 if the FP32 screen is usable
+__global__ void knn_pack_f32_kernel(const double *__restrict__ X, int64_t n, int d, int df,
+                                    const double *__restrict__ lo, const double *__restrict__ hi,
+                                    float *__restrict__ Xf, double *__restrict__ params) {
+    double Mp = 0;
+    bool ok = true;
+    for (int c = 0; c < d; c++) {
+        double l = lo[c], h = hi[c];
+        if (!(l <= h) || !(h - l < 1e300)) ok = false;
+        double half = (h - l) * 0.5;
+        Mp = half > Mp ? half : Mp;
+    }
+    ok = ok && Mp <= 1e15;
+    HDB_GRID_STRIDE(t, n * df) {
+        int64_t r = t / df;
+        int c = (int)(t - r * df);
+        float v = 0.0f;
+        if (c < d && ok) {
+            double ctr = lo[c] + (hi[c] - lo[c]) * 0.5;
+            v = (float)(X[r * d + c] - ctr);
+        }
+        Xf[t] = v;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // |x - ctr| <= M' (+ rounding of ctr): pad M' by 1e-12 relative
+        params[0] = sqrt((double)d) * 4.0 * 5.9604644775390625e-08 * (Mp * (1.0 + 1e-12)) * 1.01 + 1e-300;
+        params[1] = ok ? 1.0 : 0.0;
+    }
+}
+
 // merge S partial squared-domain lists per query and finalize (sqrt, MAX padding)
 template <int K, bool IDX>
 __global__ void knn_merge_kernel(const double *__restrict__ part_v, const int32_t *__restrict__ part_i,
@@ -320,27 +512,39 @@ static KnnPlan plan_knn(hdb_ctx *ctx, int64_t n, int Q) {
     return p;
 }
 
+// FP32-screen state for the current call (set by knn_lists_device)
+struct F32Screen {
+    const float *Xf = nullptr;
+    const double *params = nullptr;
+    bool on = false;
+};
+static thread_local F32Screen g_screen;
+
 template <int D, int K, int Q, bool EXCL, bool IDX>
 static void launch_knn_sq(hdb_ctx *ctx, const double *Xp, int64_t n, double *out_v, int32_t *out_i) {
     constexpr int DP = (D + 1) & ~1;
+    constexpr int DF = D <= 4 ? 4 : (D <= 8 ? 8 : 16);
     constexpr int U = (D <= 4) ? 4 : 2;
     KnnPlan p = plan_knn(ctx, n, Q);
     dim3 grid(p.tiles, p.S);
-    if (p.S == 1) {
-        KernelTimer t(ctx, "knn_sq");
-        hipLaunchKernelGGL((knn_sq_kernel<D, DP, K, Q, U, EXCL, IDX>), grid, dim3(256), 0, ctx->stream, Xp, n,
-                           p.chunk, out_v, out_i, 1);
-        HIP_CHECK(hipGetLastError());
-        return;
+    const bool f32 = g_screen.on;
+    double *pv = out_v;
+    int32_t *pi = out_i;
+    if (p.S > 1) {
+        pv = (double *)arena(ctx, A_WORK2, sizeof(double) * (size_t)(p.S * n * K));
+        pi = IDX ? (int32_t *)arena(ctx, A_WORK3, sizeof(int32_t) * (size_t)(p.S * n * K)) : nullptr;
     }
-    double *pv = (double *)arena(ctx, A_WORK2, sizeof(double) * (size_t)(p.S * n * K));
-    int32_t *pi = IDX ? (int32_t *)arena(ctx, A_WORK3, sizeof(int32_t) * (size_t)(p.S * n * K)) : nullptr;
     {
         KernelTimer t(ctx, "knn_sq");
-        hipLaunchKernelGGL((knn_sq_kernel<D, DP, K, Q, U, EXCL, IDX>), grid, dim3(256), 0, ctx->stream, Xp, n,
-                           p.chunk, pv, pi, 0);
+        if (f32)
+            hipLaunchKernelGGL((knn_f32x_kernel<D, DF, DP, K, Q, U, EXCL, IDX>), grid, dim3(256), 0, ctx->stream,
+                               g_screen.Xf, Xp, g_screen.params, n, p.chunk, pv, pi, p.S == 1 ? 1 : 0);
+        else
+            hipLaunchKernelGGL((knn_sq_kernel<D, DP, K, Q, U, EXCL, IDX>), grid, dim3(256), 0, ctx->stream, Xp, n,
+                               p.chunk, pv, pi, p.S == 1 ? 1 : 0);
         HIP_CHECK(hipGetLastError());
     }
+    if (p.S == 1) return;
     int g = (int)std::min<int64_t>(ceil_div(n, 256), 4096);
     hipLaunchKernelGGL((knn_merge_kernel<K, IDX>), dim3(g), dim3(256), 0, ctx->stream, pv, pi, n, p.S, out_v,
                        out_i);
@@ -391,8 +595,29 @@ void knn_lists_device(hdb_ctx *ctx, const double *X_dev, int64_t n, int d, int k
     if (n == 0) return;
     if (metric == HDB_METRIC_EUCLIDEAN) {
         int dp = (d + 1) & ~1;
-        double *Xp = (double *)arena(ctx, A_PAD, sizeof(double) * (size_t)(n * dp));
+        int df = d <= 4 ? 4 : (d <= 8 ? 8 : 16);
+        // carve: Xp (FP64 padded) | Xf (FP32 shifted) | bbox lo/hi | params
+        size_t b_xp = ((sizeof(double) * (size_t)(n * dp)) + 255) & ~size_t(255);
+        size_t b_xf = ((sizeof(float) * (size_t)(n * df)) + 255) & ~size_t(255);
+        char *base = (char *)arena(ctx, A_PAD, b_xp + b_xf + 1024 + 64 * 16);
+        double *Xp = (double *)base;
+        float *Xf = (float *)(base + b_xp);
+        double *blo = (double *)(base + b_xp + b_xf), *bhi = blo + 64, *prm = bhi + 64;
         pack_rows(ctx, X_dev, n, d, dp, Xp);
+        g_screen = F32Screen();
+        if (d <= 16 && !ctx->force_fp64) {
+            hipLaunchKernelGGL(knn_bbox_kernel, dim3(d), dim3(256), 0, ctx->stream, X_dev, n, d, blo, bhi);
+            int g = (int)std::min<int64_t>(ceil_div(n * df, 256), 8192);
+            hipLaunchKernelGGL(knn_pack_f32_kernel, dim3(g), dim3(256), 0, ctx->stream, X_dev, n, d, df, blo, bhi, Xf,
+                               prm);
+            HIP_CHECK(hipGetLastError());
+            double h_ok = 0;
+            HIP_CHECK(hipMemcpyAsync(&h_ok, prm + 1, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+            HIP_CHECK(hipStreamSynchronize(ctx->stream));
+            g_screen.on = h_ok == 1.0;
+            g_screen.Xf = Xf;
+            g_screen.params = prm;
+        }
         bool ok;
         if (lists_i) ok = excl ? dispatch_d<true, true>(ctx, d, KC, Xp, n, lists_v, lists_i)
                                : dispatch_d<false, true>(ctx, d, KC, Xp, n, lists_v, lists_i);

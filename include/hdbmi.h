@@ -66,6 +66,9 @@ int hdb_ctx_set_timing(hdb_ctx *ctx, int enable);
  * since the last reset, then resets that accumulator when reset != 0. */
 int hdb_ctx_kernel_time(hdb_ctx *ctx, const char *name, double *ms_total, int64_t *launches, int reset);
 int hdb_ctx_synchronize(hdb_ctx *ctx);
+/* Tuning/diagnostic switches: "knn_fp32_screen" (default 1) = K1 screens pairs in FP32
+ * with a rigorous bound before the exact FP64 test (results identical either way). */
+int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value);
 const char *hdb_last_error(void);
 int hdb_version(void);
 

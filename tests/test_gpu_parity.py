@@ -376,3 +376,24 @@ def test_errors_map_to_reference_exceptions(pkg, star):
         star.calculateCoreDistances(np.zeros((10, 3)), 0)  # minPts < 1
     with pytest.raises(pkg.HdbError):
         star.calculateCoreDistances(np.zeros((10, 3)), 40)  # > 32 unsupported
+
+
+# ------------------------------------------------- K1 FP32 screen (exactness)
+@pytest.mark.parametrize("scale", [1e-8, 1.0, 1e6, 1e17])
+def test_knn_fp32_screen_equals_fp64_path(pkg, oracle, scale):
+    """The FP32 screen only skips provably rejected pairs: both K1 paths equal the oracle
+    (including huge magnitudes, where the screen disables itself, and near-duplicates)."""
+    rng = np.random.default_rng(int(np.log10(scale) + 20))
+    X = blobs(4000, 3, 5, 3) * scale + 12345.0 * scale
+    X[100:140] = X[99]  # exact duplicates
+    X[200:240] = X[199] + rng.normal(size=(40, 3)) * scale * 1e-9  # near-duplicates
+    ctx = pkg.Context.get(0)
+    star = pkg.HDBSCANStar(ctx)
+    for sem in range(3):
+        ref = oracle.core_distances(X, 4, semantics=sem)
+        ctx.set_option("knn_fp32_screen", 1)
+        a = star.calculateCoreDistances(X, 4, None, sem)
+        ctx.set_option("knn_fp32_screen", 0)
+        b = star.calculateCoreDistances(X, 4, None, sem)
+        ctx.set_option("knn_fp32_screen", 1)
+        assert eq(a, ref) and eq(b, ref), sem
