@@ -144,97 +144,202 @@ __device__ __forceinline__ bool key_less(double w, int32_t lo, int32_t hi, const
     return hi < b.hi;
 }
 
+// BVH over the Morton-ordered tiles: level 0 = tiles (64 points), level L node i covers
+// level L-1 nodes 8i .. 8i+7.  Node boxes are fixed; node component tags (uniform
+// component id or -1) are rebuilt every round.
+constexpr int FAN = 8;
+constexpr int MAXLEV = 12;
+struct Bvh {
+    double *lo, *hi;      // [total_nodes][D]
+    int32_t *tag;         // [total_nodes]
+    int64_t off[MAXLEV + 1];
+    int64_t cnt[MAXLEV];
+    int levels;
+};
+
 template <int D>
-__global__ __launch_bounds__(256) void boruvka_scan_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
-                                                           const double *__restrict__ tlo,
-                                                           const double *__restrict__ thi,
-                                                           const int32_t *__restrict__ tcomp,
-                                                           unsigned long long *__restrict__ comp_w,
-                                                           double *__restrict__ best_w, int32_t *__restrict__ best_lo,
-                                                           int32_t *__restrict__ best_hi) {
-    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+__global__ void bvh_box_kernel(double *__restrict__ lo, double *__restrict__ hi, int64_t child_off, int64_t child_cnt,
+                               int64_t off, int64_t cnt) {
+    HDB_GRID_STRIDE(i, cnt) {
+        int64_t c0 = i * FAN, c1 = min(c0 + FAN, child_cnt);
+        for (int c = 0; c < D; c++) {
+            double l = INFINITY, h = -INFINITY;
+            for (int64_t k = c0; k < c1; k++) {
+                double a = lo[(child_off + k) * D + c], b = hi[(child_off + k) * D + c];
+                l = a < l ? a : l;
+                h = b > h ? b : h;
+            }
+            lo[(off + i) * D + c] = l;
+            hi[(off + i) * D + c] = h;
+        }
+    }
+}
+
+__global__ void bvh_tag_kernel(int32_t *__restrict__ tag, int64_t child_off, int64_t child_cnt, int64_t off,
+                               int64_t cnt) {
+    HDB_GRID_STRIDE(i, cnt) {
+        int64_t c0 = i * FAN, c1 = min(c0 + FAN, child_cnt);
+        int32_t t = tag[child_off + c0];
+        for (int64_t k = c0 + 1; k < c1 && t >= 0; k++)
+            if (tag[child_off + k] != t) t = -1;
+        tag[off + i] = t;
+    }
+}
+
+// lane lower bound (squared) from point x to a box
+template <int D>
+__device__ __forceinline__ double box_lb2(const double (&x)[D], const double *__restrict__ l,
+                                          const double *__restrict__ h) {
+    double lb = 0;
+#pragma unroll
+    for (int c = 0; c < D; c++) {
+        double a = l[c], b = h[c];
+        double g = x[c] < a ? a - x[c] : (x[c] > b ? x[c] - b : 0.0);
+        lb = lb + g * g;
+    }
+    return lb;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
+                                                          Bvh bvh, unsigned long long *__restrict__ comp_w,
+                                                          double *__restrict__ best_w, int32_t *__restrict__ best_lo,
+                                                          int32_t *__restrict__ best_hi) {
+    __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
+    const int w = threadIdx.x >> 6;
+    const int64_t t = (int64_t)blockIdx.x * 4 + w;
     if (t >= ntiles) return;
     const int lane = threadIdx.x & 63;
+    int32_t *stk = stack_s[w];
     const int64_t i = t * BT + lane;
     const bool valid = i < n;
-    Rec<D> me;
-    if (valid) me = recs[i];
-    else {
-        for (int c = 0; c < D; c++) me.x[c] = 0;
-        me.core = 0;
-        me.comp = -3;
-        me.id = 0;
+    double mx[D];
+    double mcore = 0;
+    int32_t mcomp = -3, mid = 0;
+    if (valid) {
+        const Rec<D> r = recs[i];
+#pragma unroll
+        for (int c = 0; c < D; c++) mx[c] = r.x[c];
+        mcore = r.core;
+        mcomp = r.comp;
+        mid = r.id;
+    } else {
+#pragma unroll
+        for (int c = 0; c < D; c++) mx[c] = 0;
     }
     Best b{INFINITY, INT32_MAX, INT32_MAX};
-    double cbound = INFINITY;  // component bound (stale-safe)
-    unsigned visits = 0;
-    const int64_t ntl = ntiles;
-    for (int64_t k = 0; k < 2 * ntl; k++) {
-        // outward order: t, t+1, t-1, t+2, t-2, ...
-        int64_t off = (k + 1) >> 1;
-        int64_t j = (k & 1) ? t + off : t - off;
-        if (k == 0) j = t;
-        if (j < 0 || j >= ntl) {
-            if (t + off >= ntl && t - off < 0) break;
-            continue;
-        }
-        // does this lane need tile j?
-        bool need = valid;
-        const int32_t tc = tcomp[j];
-        if (tc >= 0 && tc == me.comp) need = false;
-        if (need && (visits++ & 15) == 0) {
-            unsigned long long cw = __hip_atomic_load(&comp_w[me.comp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    double cbound = INFINITY;
+    // query tile box (uniform) for the visit order
+    const double *qlo = bvh.lo + t * D, *qhi = bvh.hi + t * D;
+    auto refresh = [&]() {
+        if (valid) {
+            unsigned long long cw = __hip_atomic_load(&comp_w[mcomp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             double cwd = __longlong_as_double((long long)cw);
             if (cwd < cbound) cbound = cwd;
         }
+    };
+    auto lane_needs = [&](int64_t node) -> bool {
+        if (!valid) return false;
+        const int32_t tg = bvh.tag[node];
+        if (tg >= 0 && tg == mcomp) return false;
         double bound = b.w < cbound ? b.w : cbound;
-        if (need) {
-            if (bound < INFINITY) {
-                double lb = 0;
-                for (int c = 0; c < D; c++) {
-                    double l = tlo[j * D + c], h = thi[j * D + c];
-                    double g = me.x[c] < l ? l - me.x[c] : (me.x[c] > h ? me.x[c] - h : 0.0);
-                    lb = lb + g * g;
-                }
-                // mrd >= sqrt(s) >= sqrt(lb) up to rounding: prune with a relative margin
-                if (lb * (1.0 - 1e-12) > bound * bound) need = false;
-            }
-        }
-        if (!__any(need)) continue;
-        const int64_t j0 = j * BT;
-        const int64_t j1 = min(j0 + BT, n);
-        for (int64_t q = j0; q < j1; q++) {
-            const Rec<D> &r = recs[q];  // uniform -> scalar loads
-            if (!need) continue;
-            if (r.comp == me.comp) continue;
-            double s = sq_diff(me.x[0], r.x[0]);
+        if (!(bound < INFINITY)) return true;
+        double lb = box_lb2<D>(mx, bvh.lo + node * D, bvh.hi + node * D);
+        return !(lb * (1.0 - 1e-12) > bound * bound);
+    };
+    int sp = 0;
+    if (lane == 0) stk[0] = ((bvh.levels - 1) << 26) | 0;
+    sp = 1;
+    int visits = 0;
+    while (sp > 0) {
+        __builtin_amdgcn_wave_barrier();
+        const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
+        sp--;
+        const int lev = code >> 26;
+        const int64_t idx = code & ((1 << 26) - 1);
+        const int64_t node = bvh.off[lev] + idx;
+        if ((visits++ & 7) == 0) refresh();
+        if (!__any(lane_needs(node))) continue;
+        if (lev == 0) {
+            // leaf: 64 candidates of tile idx
+            const bool need = lane_needs(node);
+            const int64_t j0 = idx * BT, j1 = min(j0 + BT, n);
+            for (int64_t q = j0; q < j1; q++) {
+                const Rec<D> &r = recs[q];  // uniform -> scalar loads
+                if (!need) continue;
+                if (r.comp == mcomp) continue;
+                double s = sq_diff(mx[0], r.x[0]);
 #pragma unroll
-            for (int c = 1; c < D; c++) s = s + sq_diff(me.x[c], r.x[c]);
-            // s > fl(b*b)*(1+2^-48) proves fl(sqrt(s)) > b strictly (a tie could still win on ids)
-            double thr = (b.w * b.w) * 1.0000000000000036;
-            if (s > thr) continue;
-            double mrd = sqrt(s);  // HDBSCANStar.java:162-168 order
-            if (me.core > mrd) mrd = me.core;
-            if (r.core > mrd) mrd = r.core;
-            int32_t lo = me.id < r.id ? me.id : r.id;
-            int32_t hi = me.id < r.id ? r.id : me.id;
-            if (key_less(mrd, lo, hi, b)) {
-                b.w = mrd;
-                b.lo = lo;
-                b.hi = hi;
+                for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
+                // s > fl(b*b)*(1+2^-48) proves fl(sqrt(s)) > b strictly (ties could still win on ids)
+                double thr = (b.w * b.w) * 1.0000000000000036;
+                if (s > thr) continue;
+                double mrd = sqrt(s);  // HDBSCANStar.java:162-168 order
+                if (mcore > mrd) mrd = mcore;
+                if (r.core > mrd) mrd = r.core;
+                int32_t lo = mid < r.id ? mid : r.id;
+                int32_t hi = mid < r.id ? r.id : mid;
+                if (key_less(mrd, lo, hi, b)) {
+                    b.w = mrd;
+                    b.lo = lo;
+                    b.hi = hi;
+                }
+            }
+            if (need && b.w < cbound) {
+                atomicMin(&comp_w[mcomp], (unsigned long long)dbits(b.w));
+                cbound = b.w;
+            }
+            continue;
+        }
+        // internal: push needed children, farthest first (nearest popped first)
+        const int64_t c0 = idx * FAN;
+        const int64_t c1 = min(c0 + FAN, bvh.cnt[lev - 1]);
+        double key[FAN];
+        bool ok[FAN];
+#pragma unroll
+        for (int k = 0; k < FAN; k++) {
+            ok[k] = false;
+            key[k] = INFINITY;
+            const int64_t c = c0 + k;
+            if (c < c1) {
+                const int64_t cn = bvh.off[lev - 1] + c;
+                ok[k] = __any(lane_needs(cn));
+                // box-to-box distance between the query tile and the child (uniform)
+                double kk = 0;
+                const double *cl = bvh.lo + cn * D, *ch = bvh.hi + cn * D;
+#pragma unroll
+                for (int d = 0; d < D; d++) {
+                    double g = qhi[d] < cl[d] ? cl[d] - qhi[d] : (ch[d] < qlo[d] ? qlo[d] - ch[d] : 0.0);
+                    kk = kk + g * g;
+                }
+                key[k] = kk;
             }
         }
-        // publish improvements of the component bound early
-        if (need && b.w < cbound) {
-            atomicMin(&comp_w[me.comp], (unsigned long long)dbits(b.w));
-            cbound = b.w;
+        // selection: push in decreasing key order
+#pragma unroll 1
+        for (int r = 0; r < FAN; r++) {
+            int sel = -1;
+            double sk = -1.0;
+#pragma unroll
+            for (int k = 0; k < FAN; k++)
+                if (ok[k] && key[k] > sk) {
+                    sk = key[k];
+                    sel = k;
+                }
+            sel = __builtin_amdgcn_readfirstlane(sel);
+            if (sel < 0) break;
+#pragma unroll
+            for (int k = 0; k < FAN; k++)
+                if (k == sel) ok[k] = false;
+            if (lane == 0) stk[sp] = ((lev - 1) << 26) | (int32_t)(c0 + sel);
+            sp++;
         }
     }
     if (valid) {
         best_w[i] = b.w;
         best_lo[i] = b.lo;
         best_hi[i] = b.hi;
-        if (b.w < INFINITY) atomicMin(&comp_w[me.comp], (unsigned long long)dbits(b.w));
+        if (b.w < INFINITY) atomicMin(&comp_w[mcomp], (unsigned long long)dbits(b.w));
     }
 }
 
@@ -350,16 +455,33 @@ static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double 
                          double *w) {
     if (n > INT32_MAX / 2) HDB_THROW(HDB_EINVAL, "n too large");
     const int64_t ntiles = ceil_div(n, BT);
+    Bvh bvh;
+    {
+        int64_t c = ntiles, tot = 0;
+        bvh.levels = 0;
+        while (true) {
+            if (bvh.levels >= MAXLEV) HDB_THROW(HDB_EINVAL, "boruvka: too many BVH levels");
+            bvh.off[bvh.levels] = tot;
+            bvh.cnt[bvh.levels] = c;
+            tot += c;
+            bvh.levels++;
+            if (c == 1) break;
+            c = ceil_div(c, FAN);
+        }
+        bvh.off[bvh.levels] = tot;
+    }
+    const int64_t nnodes = bvh.off[bvh.levels];
     size_t off = 0;
     auto carve = [&](size_t bytes) {
         size_t o = off;
         off += (bytes + 255) & ~size_t(255);
         return o;
     };
+    size_t o_blo = carve(sizeof(double) * D * nnodes), o_bhi = carve(sizeof(double) * D * nnodes),
+           o_btag = carve(4 * nnodes);
     size_t o_lo = carve(sizeof(double) * 64), o_hi = carve(sizeof(double) * 64), o_keys = carve(8 * n),
            o_keys2 = carve(8 * n), o_iota = carve(4 * n), o_perm = carve(4 * n), o_recs = carve(sizeof(Rec<D>) * n),
-           o_inv = carve(4 * n), o_tlo = carve(sizeof(double) * D * ntiles), o_thi = carve(sizeof(double) * D * ntiles),
-           o_tc = carve(4 * ntiles), o_cw = carve(8 * n), o_ck = carve(8 * n), o_bw = carve(8 * n), o_bl = carve(4 * n),
+           o_inv = carve(4 * n), o_cw = carve(8 * n), o_ck = carve(8 * n), o_bw = carve(8 * n), o_bl = carve(4 * n),
            o_bh = carve(4 * n), o_par = carve(4 * n), o_par2 = carve(4 * n), o_root = carve(4 * n), o_ne = carve(8),
            o_chg = carve(8), o_ea = carve(4 * n), o_eb = carve(4 * n), o_ew = carve(8 * n);
     char *base = (char *)arena(ctx, A_WORK0, off);
@@ -368,8 +490,11 @@ static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double 
     uint64_t *keys = (uint64_t *)P(o_keys), *keys2 = (uint64_t *)P(o_keys2);
     int32_t *iota = (int32_t *)P(o_iota), *perm = (int32_t *)P(o_perm), *inv = (int32_t *)P(o_inv);
     Rec<D> *recs = (Rec<D> *)P(o_recs);
-    double *tlo = (double *)P(o_tlo), *thi = (double *)P(o_thi);
-    int32_t *tcomp = (int32_t *)P(o_tc);
+    bvh.lo = (double *)P(o_blo);
+    bvh.hi = (double *)P(o_bhi);
+    bvh.tag = (int32_t *)P(o_btag);
+    double *tlo = bvh.lo, *thi = bvh.hi;  // level 0 = tiles
+    int32_t *tcomp = bvh.tag;
     unsigned long long *comp_w = (unsigned long long *)P(o_cw), *comp_key = (unsigned long long *)P(o_ck);
     double *best_w = (double *)P(o_bw);
     int32_t *best_lo = (int32_t *)P(o_bl), *best_hi = (int32_t *)P(o_bh);
@@ -392,6 +517,9 @@ static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double 
     }
     hipLaunchKernelGGL(build_recs_kernel<D>, dim3(g), dim3(256), 0, st, X, core, perm, n, recs, inv);
     hipLaunchKernelGGL(tile_box_kernel<D>, dim3((unsigned)ntiles), dim3(64), 0, st, recs, n, tlo, thi);
+    for (int L = 1; L < bvh.levels; L++)
+        hipLaunchKernelGGL(bvh_box_kernel<D>, dim3((unsigned)std::min<int64_t>(ceil_div(bvh.cnt[L], 256), 4096)), dim3(256),
+                           0, st, bvh.lo, bvh.hi, bvh.off[L - 1], bvh.cnt[L - 1], bvh.off[L], bvh.cnt[L]);
     HIP_CHECK(hipMemsetAsync(n_edges, 0, 8, st));
     HIP_CHECK(hipGetLastError());
 
@@ -399,12 +527,15 @@ static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double 
     for (int round = 0; have < n - 1; round++) {
         if (round > 64) HDB_THROW(HDB_EINVAL, "boruvka did not converge (non-finite distances?)");
         hipLaunchKernelGGL(tile_comp_kernel<D>, dim3((unsigned)ntiles), dim3(64), 0, st, recs, n, tcomp);
+        for (int L = 1; L < bvh.levels; L++)
+            hipLaunchKernelGGL(bvh_tag_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(bvh.cnt[L], 256), 4096)),
+                               dim3(256), 0, st, bvh.tag, bvh.off[L - 1], bvh.cnt[L - 1], bvh.off[L], bvh.cnt[L]);
         HIP_CHECK(hipMemsetAsync(comp_w, 0xff, 8 * n, st));
         HIP_CHECK(hipMemsetAsync(comp_key, 0xff, 8 * n, st));
         {
             KernelTimer ts(ctx, "boruvka_scan");
-            hipLaunchKernelGGL(boruvka_scan_kernel<D>, dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, st, recs, n,
-                               ntiles, tlo, thi, tcomp, comp_w, best_w, best_lo, best_hi);
+            hipLaunchKernelGGL(boruvka_bvh_kernel<D>, dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, st, recs, n,
+                               ntiles, bvh, comp_w, best_w, best_lo, best_hi);
         }
         hipLaunchKernelGGL(comp_key_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, comp_w, best_w, best_lo, best_hi,
                            comp_key);

@@ -224,29 +224,43 @@ __global__ __launch_bounds__(256) void knn_f32x_kernel(const float *__restrict__
         }
         thr[q] = INFINITY;
     }
-    int64_t a = c_hi, b = c_hi;
-    if (EXCL) {
-        a = max(c_lo, min(c_hi, q0));
-        b = max(a, min(c_hi, qhi));
-    }
+    // exact FP64 test of one pair (reference operation order) + insertion
+    auto exact = [&](int q, const double (&cc)[D], int64_t jcand, bool self_chk) {
+        double acc = sq_diff(xq[q][0], cc[0]);
+#pragma unroll
+        for (int c = 1; c < D; c++) acc = acc + sq_diff(xq[q][c], cc[c]);
+        if (self_chk && qi[q] == jcand) acc = INFINITY;
+        if (acc < buf[q][K - 1]) {
+            if (IDX) topk_insert_idx<K>(buf[q], bidx[q], acc, (int)jcand);
+            else topk_insert<K>(buf[q], acc);
+            thr[q] = knn_thr32(buf[q][K - 1], E);
+        }
+    };
+    auto exact_range = [&](int64_t lo, int64_t hi, bool self_chk) {
 #pragma unroll 1
-    for (int seg = 0; seg < 3; seg++) {
-        int64_t s_lo = seg == 0 ? c_lo : (seg == 1 ? a : b);
-        int64_t s_hi = seg == 0 ? a : (seg == 1 ? b : c_hi);
-        const bool chk = EXCL && seg == 1;
-        int64_t j = s_lo;
+        for (int64_t j = lo; j < hi; j++) {
+            const double *cr = Xp + j * DP;
+            double cc[D];
+#pragma unroll
+            for (int c = 0; c < D; c++) cc[c] = cr[c];
+#pragma unroll
+            for (int q = 0; q < Q; q++) exact(q, cc, j, self_chk);
+        }
+    };
+    // screened range: full groups of U candidates, FP32 test per pair, exact re-test only
+    // for the (candidate, query) pairs some lane screened in
+    auto screened_range = [&](int64_t lo, int64_t hi) {
+        const int64_t ng = (hi - lo) / U;
+        const float *cp = Xf + lo * DF;
 #pragma unroll 1
-        for (; j < s_hi; j += U) {
-            const int64_t ucount = min((int64_t)U, s_hi - j);
-            // FP32 screen
-            bool hit = false;
+        for (int64_t g = 0; g < ng; g++, cp += U * DF) {
+            bool pass[U][Q];
+            bool any = false;
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const int64_t jj = j + u < s_hi ? j + u : j;  // clamp (masked below)
-                const float *cr = Xf + jj * DF;
                 float cf[D];
 #pragma unroll
-                for (int c = 0; c < D; c++) cf[c] = cr[c];
+                for (int c = 0; c < D; c++) cf[c] = cp[u * DF + c];
 #pragma unroll
                 for (int q = 0; q < Q; q++) {
                     float t0 = xf[q][0] - cf[0];
@@ -256,34 +270,37 @@ __global__ __launch_bounds__(256) void knn_f32x_kernel(const float *__restrict__
                         float t = xf[q][c] - cf[c];
                         acc = __builtin_fmaf(t, t, acc);
                     }
-                    bool ok = u < ucount && !(acc >= thr[q]);
-                    if (chk && qi[q] == jj) ok = false;
-                    hit |= ok;
+                    pass[u][q] = !(acc >= thr[q]);
+                    any |= pass[u][q];
                 }
             }
-            if (!hit) continue;
-            // exact FP64 path for the group (reference operation order)
+            if (!any) continue;
+            const int64_t j = lo + g * U;
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                if (u >= ucount) break;
+                bool pu = false;
+#pragma unroll
+                for (int q = 0; q < Q; q++) pu |= pass[u][q];
+                if (!pu) continue;
                 const double *cr = Xp + (j + u) * DP;
                 double cc[D];
 #pragma unroll
                 for (int c = 0; c < D; c++) cc[c] = cr[c];
 #pragma unroll
-                for (int q = 0; q < Q; q++) {
-                    double acc = sq_diff(xq[q][0], cc[0]);
-#pragma unroll
-                    for (int c = 1; c < D; c++) acc = acc + sq_diff(xq[q][c], cc[c]);
-                    if (chk && qi[q] == j + u) acc = INFINITY;
-                    if (acc < buf[q][K - 1]) {
-                        if (IDX) topk_insert_idx<K>(buf[q], bidx[q], acc, (int)(j + u));
-                        else topk_insert<K>(buf[q], acc);
-                        thr[q] = knn_thr32(buf[q][K - 1], E);
-                    }
-                }
+                for (int q = 0; q < Q; q++)
+                    if (pass[u][q]) exact(q, cc, j + u, false);
             }
         }
+        exact_range(lo + ng * U, hi, false);  // tail
+    };
+    if (EXCL) {
+        const int64_t a = max(c_lo, min(c_hi, q0));
+        const int64_t b = max(a, min(c_hi, qhi));
+        screened_range(c_lo, a);
+        exact_range(a, b, true);  // the query tile itself: self pairs excluded
+        screened_range(b, c_hi);
+    } else {
+        screened_range(c_lo, c_hi);
     }
 #pragma unroll
     for (int q = 0; q < Q; q++) {
