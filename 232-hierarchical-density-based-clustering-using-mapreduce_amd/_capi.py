@@ -12,7 +12,7 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libhdbmi.so")
+LIB_PATH = os.environ.get("HDBMI_LIB") or os.path.join(HERE, "lib", "libhdbmi.so")  # override: A/B builds
 
 HDB_OK = 0
 ERRORS = {

@@ -13,14 +13,15 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-OUT = os.path.join(HERE, "lib")
+OUT = os.environ.get("HDBMI_OUT") or os.path.join(HERE, "lib")
 LIB = os.path.join(OUT, "libhdbmi.so")
 SOURCES = ["context.cpp", "capi.cpp", "local_model.cpp", "knn.hip", "nearest.hip", "prim.hip",
            "bubbles.hip", "merge.hip", "boruvka.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # -ffp-contract=off: the reference (Java) never fuses a*b+c; bit-exact parity needs the same.
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
+FLAGS = [*os.environ.get("HDBMI_EXTRA_FLAGS", "").split(),
+         "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
          "--offload-arch=gfx950", "-munsafe-fp-atomics", "-Wno-unused-result"]
 
 

@@ -247,51 +247,89 @@ __global__ __launch_bounds__(256) void knn_f32x_kernel(const float *__restrict__
             for (int q = 0; q < Q; q++) exact(q, cc, j, self_chk);
         }
     };
-    // screened range: full groups of U candidates, FP32 test per pair, exact re-test only
-    // for the (candidate, query) pairs some lane screened in
+    // screened range, candidates staged through LDS: the block's 4 waves share every chunk
+    // of CH candidates (FP32, DF floats each) -- one coalesced global load per thread per
+    // chunk, double-buffered, one barrier per chunk; waves read candidates with broadcast
+    // ds_reads (in order, so reads run ahead of use).  FP32 test per pair; the exact FP64
+    // re-test runs only for (candidate, query) pairs some lane screened in.
+    constexpr int CH = 256;
+    constexpr int V4 = DF / 4;  // float4 per candidate
+    __shared__ float4 sc[2][CH * V4];
     auto screened_range = [&](int64_t lo, int64_t hi) {
-        const int64_t ng = (hi - lo) / U;
-        const float *cp = Xf + lo * DF;
+        if (lo >= hi) return;
+        const int64_t nch = (hi - lo + CH - 1) / CH;
+        float4 pre[V4];
+        auto prefetch = [&](int64_t k) {
+            const int64_t j = lo + k * CH + threadIdx.x;
+            const float4 *src = reinterpret_cast<const float4 *>(Xf + (j < hi ? j : lo) * DF);
+#pragma unroll
+            for (int v = 0; v < V4; v++) pre[v] = src[v];
+        };
+        auto stage = [&](int buf) {
+#pragma unroll
+            for (int v = 0; v < V4; v++) sc[buf][threadIdx.x * V4 + v] = pre[v];
+        };
+        prefetch(0);
+        stage(0);
+        __syncthreads();
 #pragma unroll 1
-        for (int64_t g = 0; g < ng; g++, cp += U * DF) {
-            bool pass[U][Q];
-            bool any = false;
+        for (int64_t k = 0; k < nch; k++) {
+            const int buf = (int)(k & 1);
+            if (k + 1 < nch) prefetch(k + 1);
+            const int64_t jb = lo + k * CH;
+            const int cnt = (int)min((int64_t)CH, hi - jb);
+            const int ng = cnt / U;
+#pragma unroll 1
+            for (int g = 0; g < ng; g++) {
+                bool pass[U][Q];
+                bool any = false;
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                float cf[D];
+                for (int u = 0; u < U; u++) {
+                    const float4 c4 = sc[buf][(g * U + u) * V4];
+                    float cf[D];
 #pragma unroll
-                for (int c = 0; c < D; c++) cf[c] = cp[u * DF + c];
-#pragma unroll
-                for (int q = 0; q < Q; q++) {
-                    float t0 = xf[q][0] - cf[0];
-                    float acc = t0 * t0;
-#pragma unroll
-                    for (int c = 1; c < D; c++) {
-                        float t = xf[q][c] - cf[c];
-                        acc = __builtin_fmaf(t, t, acc);
+                    for (int c = 0; c < D; c++) {
+                        if (c < 4) cf[c] = c == 0 ? c4.x : (c == 1 ? c4.y : (c == 2 ? c4.z : c4.w));
+                        else {
+                            const float4 e = sc[buf][(g * U + u) * V4 + c / 4];
+                            const int r = c & 3;
+                            cf[c] = r == 0 ? e.x : (r == 1 ? e.y : (r == 2 ? e.z : e.w));
+                        }
                     }
-                    pass[u][q] = !(acc >= thr[q]);
-                    any |= pass[u][q];
+#pragma unroll
+                    for (int q = 0; q < Q; q++) {
+                        float t0 = xf[q][0] - cf[0];
+                        float acc = t0 * t0;
+#pragma unroll
+                        for (int c = 1; c < D; c++) {
+                            float t = xf[q][c] - cf[c];
+                            acc = __builtin_fmaf(t, t, acc);
+                        }
+                        pass[u][q] = !(acc >= thr[q]);
+                        any |= pass[u][q];
+                    }
+                }
+                if (!any) continue;
+                const int64_t j = jb + g * U;
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    bool pu = false;
+#pragma unroll
+                    for (int q = 0; q < Q; q++) pu |= pass[u][q];
+                    if (!pu) continue;
+                    const double *cr = Xp + (j + u) * DP;
+                    double cc[D];
+#pragma unroll
+                    for (int c = 0; c < D; c++) cc[c] = cr[c];
+#pragma unroll
+                    for (int q = 0; q < Q; q++)
+                        if (pass[u][q]) exact(q, cc, j + u, false);
                 }
             }
-            if (!any) continue;
-            const int64_t j = lo + g * U;
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                bool pu = false;
-#pragma unroll
-                for (int q = 0; q < Q; q++) pu |= pass[u][q];
-                if (!pu) continue;
-                const double *cr = Xp + (j + u) * DP;
-                double cc[D];
-#pragma unroll
-                for (int c = 0; c < D; c++) cc[c] = cr[c];
-#pragma unroll
-                for (int q = 0; q < Q; q++)
-                    if (pass[u][q]) exact(q, cc, j + u, false);
-            }
+            exact_range(jb + (int64_t)ng * U, jb + cnt, false);  // chunk tail
+            if (k + 1 < nch) stage(buf ^ 1);
+            __syncthreads();
         }
-        exact_range(lo + ng * U, hi, false);  // tail
     };
     if (EXCL) {
         const int64_t a = max(c_lo, min(c_hi, q0));
@@ -541,7 +579,14 @@ template <int D, int K, int Q, bool EXCL, bool IDX>
 static void launch_knn_sq(hdb_ctx *ctx, const double *Xp, int64_t n, double *out_v, int32_t *out_i) {
     constexpr int DP = (D + 1) & ~1;
     constexpr int DF = D <= 4 ? 4 : (D <= 8 ? 8 : 16);
-    constexpr int U = (D <= 4) ? 4 : 2;
+#ifndef HDB_KNN_U
+#define HDB_KNN_U 4
+#endif
+    constexpr int U = (D <= 4) ? HDB_KNN_U : 2;
+#ifndef HDB_KNN_US
+#define HDB_KNN_US 8
+#endif
+    constexpr int US = (D <= 4) ? HDB_KNN_US : (D <= 8 ? 4 : 2);  // screen kernel group
     KnnPlan p = plan_knn(ctx, n, Q);
     dim3 grid(p.tiles, p.S);
     const bool f32 = g_screen.on;
@@ -554,7 +599,7 @@ static void launch_knn_sq(hdb_ctx *ctx, const double *Xp, int64_t n, double *out
     {
         KernelTimer t(ctx, "knn_sq");
         if (f32)
-            hipLaunchKernelGGL((knn_f32x_kernel<D, DF, DP, K, Q, U, EXCL, IDX>), grid, dim3(256), 0, ctx->stream,
+            hipLaunchKernelGGL((knn_f32x_kernel<D, DF, DP, K, Q, US, EXCL, IDX>), grid, dim3(256), 0, ctx->stream,
                                g_screen.Xf, Xp, g_screen.params, n, p.chunk, pv, pi, p.S == 1 ? 1 : 0);
         else
             hipLaunchKernelGGL((knn_sq_kernel<D, DP, K, Q, U, EXCL, IDX>), grid, dim3(256), 0, ctx->stream, Xp, n,
@@ -568,10 +613,13 @@ static void launch_knn_sq(hdb_ctx *ctx, const double *Xp, int64_t n, double *out
     HIP_CHECK(hipGetLastError());
 }
 
+#ifndef HDB_KNN_Q
+#define HDB_KNN_Q 4
+#endif
 template <int D, int K, bool EXCL, bool IDX>
 static void dispatch_q(hdb_ctx *ctx, const double *Xp, int64_t n, double *ov, int32_t *oi) {
     // queries per lane: keep D*Q + K*Q doubles well inside the register budget
-    constexpr int Q = (D * 2 + K * (IDX ? 3 : 2) <= 24) ? 4 : ((D + K) <= 24 ? 2 : 1);
+    constexpr int Q = (D * 2 + K * (IDX ? 3 : 2) <= 24) ? HDB_KNN_Q : ((D + K) <= 24 ? 2 : 1);
     launch_knn_sq<D, K, Q, EXCL, IDX>(ctx, Xp, n, ov, oi);
 }
 

@@ -1,7 +1,7 @@
 """Micro-benchmark of K1 (and Boruvka) at config-2 size: prints kernel times, both K1 paths."""
 import importlib, sys, time, json, os
 import numpy as np
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 pkg = importlib.import_module("232-hierarchical-density-based-clustering-using-mapreduce_amd")
 from bench import make_blobs
