@@ -83,6 +83,7 @@ def lib():
             "hdb_ctx_kernel_time": [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int],
             "hdb_ctx_synchronize": [vp],
             "hdb_ctx_set_option": [vp, C.c_char_p, C.c_int64],
+            "hdb_ctx_get_stat": [vp, C.c_char_p, C.POINTER(C.c_int64)],
             "hdb_distance_rows": [vp, dp, dp, i64, i32, i32, dp],
             "hdb_core_distances": [vp, dp, i64, i32, i32, i32, i32, dp],
             "hdb_knn": [vp, dp, i64, i32, i32, i32, i32, dp, ip],
@@ -111,7 +112,7 @@ def lib():
 
 
 EXPORTED = ["hdb_ctx_create", "hdb_ctx_destroy", "hdb_ctx_set_stream", "hdb_ctx_set_timing", "hdb_ctx_set_option",
-            "hdb_ctx_kernel_time", "hdb_ctx_synchronize", "hdb_last_error", "hdb_version",
+            "hdb_ctx_get_stat", "hdb_ctx_kernel_time", "hdb_ctx_synchronize", "hdb_last_error", "hdb_version",
             "hdb_distance_rows", "hdb_core_distances", "hdb_knn", "hdb_prim_mst", "hdb_prim_mst_batched",
             "hdb_leaf_msts", "hdb_mst_boruvka", "hdb_nearest_sample", "hdb_bubble_stats",
             "hdb_bubble_core_distances", "hdb_bubble_prim_mst", "hdb_local_model", "hdb_quicksort_edges",
@@ -167,6 +168,11 @@ class Context:
 
     def set_option(self, name: str, value: int):
         check(lib().hdb_ctx_set_option(self.h, name.encode(), int(value)), "hdb_ctx_set_option")
+
+    def get_stat(self, name: str) -> int:
+        v = C.c_int64()
+        check(lib().hdb_ctx_get_stat(self.h, name.encode(), C.byref(v)), "hdb_ctx_get_stat")
+        return v.value
 
     def synchronize(self):
         check(lib().hdb_ctx_synchronize(self.h), "hdb_ctx_synchronize")

@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.environ.get("HDBMI_OUT") or os.path.join(HERE, "lib")
 LIB = os.path.join(OUT, "libhdbmi.so")
 SOURCES = ["context.cpp", "capi.cpp", "local_model.cpp", "knn.hip", "nearest.hip", "prim.hip",
-           "bubbles.hip", "merge.hip", "boruvka.hip"]
+           "bubbles.hip", "merge.hip", "spatial.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # -ffp-contract=off: the reference (Java) never fuses a*b+c; bit-exact parity needs the same.

@@ -57,6 +57,11 @@ struct hdb_ctx {
     hdb::Arena arenas[8];
     int num_cus = 256;
     bool force_fp64 = false;  // disable the FP32 screen in K1 (A/B and tests)
+    bool knn_tree = true;     // K1t (box-pruned) for euclidean lists when the shape allows
+    int64_t knn_tree_min_n = 8192;
+    bool boruvka_seed = true;  // seed Boruvka rounds from the previous round's edges
+    bool count_evals = false;  // K1t counts evaluated pairs (diagnostic; costs one sync)
+    std::map<std::string, int64_t> stats;  // diagnostic counters (count_evals)
 };
 
 namespace hdb {
@@ -196,6 +201,37 @@ __device__ __forceinline__ void argmin_last(double &v, int &i, double v2, int i2
     if (i < 0 || v2 < v || (v2 == v && i2 > i)) {
         v = v2;
         i = i2;
+    }
+}
+
+// top-K insertion network (shared by K1, K1t and the epilogues)
+// Insert x into ascending buf[0..K) if x < buf[K-1] (strict, HDBSCANStar.java:89);
+// the largest element drops out.  Predicated compare/select chain, no dynamic indexing.
+template <int K>
+__device__ __forceinline__ void topk_insert(double (&buf)[K], double x) {
+    if (x < buf[K - 1]) {
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            double b = buf[i];
+            bool lt = x < b;
+            buf[i] = lt ? x : b;
+            x = lt ? b : x;
+        }
+    }
+}
+template <int K>
+__device__ __forceinline__ void topk_insert_idx(double (&buf)[K], int (&idx)[K], double x, int xi) {
+    if (x < buf[K - 1]) {
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            double b = buf[i];
+            int bi = idx[i];
+            bool lt = x < b;
+            buf[i] = lt ? x : b;
+            idx[i] = lt ? xi : bi;
+            x = lt ? b : x;
+            xi = lt ? bi : xi;
+        }
     }
 }
 

@@ -214,11 +214,39 @@ int hdb_ctx_kernel_time(hdb_ctx *ctx, const char *name, double *ms_total, int64_
 
 int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
     if (!ctx || !name) return HDB_EINVAL;
-    if (std::string(name) == "knn_fp32_screen") {
+    const std::string k(name);
+    if (k == "knn_fp32_screen") {
         ctx->force_fp64 = value == 0;
         return HDB_OK;
     }
+    if (k == "knn_tree") {
+        ctx->knn_tree = value != 0;
+        return HDB_OK;
+    }
+    if (k == "knn_tree_min_n") {
+        ctx->knn_tree_min_n = value;
+        return HDB_OK;
+    }
+    if (k == "boruvka_seed") {
+        ctx->boruvka_seed = value != 0;
+        return HDB_OK;
+    }
+    if (k == "count_evals") {
+        ctx->count_evals = value != 0;
+        return HDB_OK;
+    }
     set_error(std::string("unknown option ") + name);
+    return HDB_EINVAL;
+}
+
+int hdb_ctx_get_stat(hdb_ctx *ctx, const char *name, int64_t *value) {
+    if (!ctx || !name || !value) return HDB_EINVAL;
+    auto it = ctx->stats.find(name);
+    if (it != ctx->stats.end()) {
+        *value = it->second;
+        return HDB_OK;
+    }
+    set_error(std::string("unknown stat ") + name);
     return HDB_EINVAL;
 }
 

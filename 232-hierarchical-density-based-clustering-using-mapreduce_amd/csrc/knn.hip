@@ -11,7 +11,7 @@
 // distance and takes the sqrt once per kept value (sqrt is monotone, so the k smallest
 // sqrt values are the sqrt of the k smallest squares).  A rare predicated insertion
 // network keeps the per-query top-K sorted in registers.
-#include "common.hpp"
+#include "internal.hpp"
 
 namespace hdb {
 
@@ -31,37 +31,6 @@ void pack_rows(hdb_ctx *ctx, const double *X, int64_t n, int d, int dp, double *
     int grid = (int)std::min<int64_t>(ceil_div(tot, 256), 8192);
     hipLaunchKernelGGL(pack_rows_kernel, dim3(grid), dim3(256), 0, ctx->stream, X, n, d, dp, Xp);
     HIP_CHECK(hipGetLastError());
-}
-
-// ------------------------------------------------------- insertion network
-// Insert x into ascending buf[0..K) if x < buf[K-1] (strict, HDBSCANStar.java:89);
-// the largest element drops out.  Predicated compare/select chain, no dynamic indexing.
-template <int K>
-__device__ __forceinline__ void topk_insert(double (&buf)[K], double x) {
-    if (x < buf[K - 1]) {
-#pragma unroll
-        for (int i = 0; i < K; i++) {
-            double b = buf[i];
-            bool lt = x < b;
-            buf[i] = lt ? x : b;
-            x = lt ? b : x;
-        }
-    }
-}
-template <int K>
-__device__ __forceinline__ void topk_insert_idx(double (&buf)[K], int (&idx)[K], double x, int xi) {
-    if (x < buf[K - 1]) {
-#pragma unroll
-        for (int i = 0; i < K; i++) {
-            double b = buf[i];
-            int bi = idx[i];
-            bool lt = x < b;
-            buf[i] = lt ? x : b;
-            idx[i] = lt ? xi : bi;
-            x = lt ? b : x;
-            xi = lt ? bi : xi;
-        }
-    }
 }
 
 // ------------------------------------------------------------ main kernel
@@ -658,6 +627,9 @@ void knn_lists_device(hdb_ctx *ctx, const double *X_dev, int64_t n, int d, int k
     if (KC < 0) HDB_THROW(HDB_EINVAL, "k too large (max 31)");
     *KC_out = KC;
     if (n == 0) return;
+    if (metric == HDB_METRIC_EUCLIDEAN && !lists_i && ctx->knn_tree && n >= ctx->knn_tree_min_n &&
+        knn_tree_device(ctx, X_dev, n, d, KC, excl, lists_v))
+        return;
     if (metric == HDB_METRIC_EUCLIDEAN) {
         int dp = (d + 1) & ~1;
         int df = d <= 4 ? 4 : (d <= 8 ? 8 : 16);

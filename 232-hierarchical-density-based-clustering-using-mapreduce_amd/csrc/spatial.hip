@@ -1,0 +1,987 @@
+// spatial.hip -- the Morton-ordered tile/BVH index over a partition and the two exact
+// traversals that use it:
+//   K1t  knn_tree_kernel    -- per-point k smallest distances (core distances, a3/a4) with
+//                              box pruning instead of all n^2 pairs;
+//   K2b  boruvka_bvh_kernel -- exact MST of the mutual-reachability graph (a5) for graphs
+//                              too large for the step-serial Prim (config 2: one 1M graph).
+//
+// K1t contract: lists bit-identical to K1 (knn.hip).  Every evaluated pair uses the same
+// FP64 expression in the reference's operation order (EuclideanDistance.java:31-33), and a
+// subtree is skipped only when its box lower bound lb satisfies lb >= the lane's current
+// K-th smallest squared distance.  With correctly rounded, monotone operations the computed
+// squared distance of any point in the box is >= the computed lb (|fl(c-x)| >= fl(a-x) for
+// c beyond the face a, squares and sums are monotone), so a skipped pair could never pass
+// the strict '<' insertion test (HDBSCANStar.java:89).  The kept values form the same
+// multiset as the brute-force scan's, independent of visit order.
+//
+// K2b contract: an MST under the strict total order (w, s, min id, max id) on edges, with
+// w = max(sqrt(s), core_p, core_q) computed with exactly the reference Prim's expression
+// (HDBSCANStar.java:162-168) and s the squared distance (see Best below).  Every MST has the same sorted weight sequence, so the
+// weights equal the reference Prim's bit-for-bit; the topology may differ from Prim's only
+// among equal-weight edges (Prim breaks ties by scan order).  Edges are returned sorted by
+// (w, min id, max id).
+//
+// Layout: points are sorted by a Morton key over (up to) the first 8 dimensions, cut into
+// 64-point tiles with a per-tile bounding box; tiles are the leaves of a fan-8 BVH whose
+// node boxes are fixed and whose per-round "uniform component" tags drive K2b.  A wave owns
+// one query tile (lane = point) and walks the BVH nearest-first with a wave-uniform stack in
+// LDS, descending into a node only when some lane still needs it.  For K2b the bound is
+// min(own best, the component's best so far), the latter read from the per-round component
+// minimum that other waves publish with atomicMin (a stale read only weakens the bound,
+// never prunes a winner: pruning needs LB > bound strictly).
+#include <hipcub/hipcub.hpp>
+
+#include "internal.hpp"
+
+namespace hdb {
+
+constexpr int BT = 64;  // tile size (one wave)
+
+template <int D>
+struct Rec {
+    double x[D];
+    double core;
+    int32_t comp;
+    int32_t id;
+};
+
+__device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
+
+// ---------------------------------------------------------------- morton
+__global__ void bbox_reduce_kernel(const double *__restrict__ X, int64_t n, int d, double *__restrict__ lo,
+                                   double *__restrict__ hi) {
+    // one block per dimension (d <= 64)
+    const int c = blockIdx.x;
+    __shared__ double sl[256], sh[256];
+    double l = INFINITY, h = -INFINITY;
+    for (int64_t i = threadIdx.x; i < n; i += 256) {
+        double v = X[i * d + c];
+        l = fmin(l, v);
+        h = fmax(h, v);
+    }
+    sl[threadIdx.x] = l;
+    sh[threadIdx.x] = h;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            sl[threadIdx.x] = fmin(sl[threadIdx.x], sl[threadIdx.x + s]);
+            sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + s]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        lo[c] = sl[0];
+        hi[c] = sh[0];
+    }
+}
+
+__global__ void morton_kernel(const double *__restrict__ X, int64_t n, int d, const double *__restrict__ lo,
+                              const double *__restrict__ hi, uint64_t *__restrict__ keys, int32_t *__restrict__ iota) {
+    const int dk = d < 8 ? d : 8;
+    const int bits = 63 / dk > 21 ? 21 : 63 / dk;
+    HDB_GRID_STRIDE(i, n) {
+        uint64_t key = 0;
+        uint32_t q[8];
+        for (int c = 0; c < dk; c++) {
+            double span = hi[c] - lo[c];
+            double t = span > 0 ? (X[i * d + c] - lo[c]) / span : 0.0;
+            t = t < 0 ? 0 : (t > 1 ? 1 : t);
+            if (t != t) t = 0;
+            q[c] = (uint32_t)(t * (double)((1u << bits) - 1));
+        }
+        for (int b = bits - 1; b >= 0; b--)
+            for (int c = 0; c < dk; c++) key = (key << 1) | ((q[c] >> b) & 1u);
+        keys[i] = key;
+        iota[i] = (int32_t)i;
+    }
+}
+
+template <int D>
+__global__ void build_recs_kernel(const double *__restrict__ X, const double *__restrict__ core,
+                                  const int32_t *__restrict__ perm, int64_t n, Rec<D> *__restrict__ recs,
+                                  int32_t *__restrict__ inv) {
+    HDB_GRID_STRIDE(i, n) {
+        int32_t o = perm[i];
+        Rec<D> r;
+        for (int c = 0; c < D; c++) r.x[c] = X[(int64_t)o * D + c];
+        r.core = core ? core[o] : 0.0;
+        r.comp = (int32_t)i;
+        r.id = o;
+        recs[i] = r;
+        inv[o] = (int32_t)i;
+    }
+}
+
+// Tile boxes (coordinates fixed) and uniform-component tags (per round).  Each 64-point
+// tile is also cut into 4 sub-groups of SG = 16 consecutive points with their own box and
+// tag: a leaf visit skips a sub-group no lane needs (finer culling, same wave shape).
+constexpr int SG = 16;
+constexpr int NSG = BT / SG;
+
+template <int D>
+__global__ void tile_box_kernel(const Rec<D> *__restrict__ recs, int64_t n, double *__restrict__ tlo,
+                                double *__restrict__ thi, double *__restrict__ slo, double *__restrict__ shi) {
+    const int64_t t = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t i = t * BT + lane;
+    for (int c = 0; c < D; c++) {
+        double v = i < n ? recs[i].x[c] : NAN;
+        double l = i < n ? v : INFINITY, h = i < n ? v : -INFINITY;
+        for (int off = SG / 2; off >= 1; off >>= 1) {
+            l = fmin(l, __shfl_xor(l, off));
+            h = fmax(h, __shfl_xor(h, off));
+        }
+        if ((lane & (SG - 1)) == 0) {
+            slo[(t * NSG + lane / SG) * D + c] = l;
+            shi[(t * NSG + lane / SG) * D + c] = h;
+        }
+        for (int off = BT / 2; off >= SG; off >>= 1) {
+            l = fmin(l, __shfl_xor(l, off));
+            h = fmax(h, __shfl_xor(h, off));
+        }
+        if (lane == 0) {
+            tlo[t * D + c] = l;
+            thi[t * D + c] = h;
+        }
+    }
+}
+
+template <int D>
+__global__ void tile_comp_kernel(const Rec<D> *__restrict__ recs, int64_t n, int32_t *__restrict__ tcomp,
+                                 int32_t *__restrict__ scomp) {
+    const int64_t t = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t i = t * BT + lane;
+    int32_t c = i < n ? recs[i].comp : -2;
+    int32_t c0 = __shfl(c, 0);
+    bool all = __all((c == c0) || (c == -2));
+    if (lane == 0) tcomp[t] = all ? c0 : -1;
+    // sub-group tags: lane g*SG holds the group's first component
+    int32_t g0 = __shfl(c, lane & ~(SG - 1));
+    unsigned long long bad = __ballot(!((c == g0) || (c == -2)));
+    if ((lane & (SG - 1)) == 0) {
+        const bool uni = ((bad >> (lane & ~(SG - 1))) & ((1ull << SG) - 1)) == 0;
+        scomp[t * NSG + lane / SG] = uni ? g0 : -1;
+    }
+}
+
+// --------------------------------------------------------------- scan
+// Edge order for K2b: (w, s, lo, hi) -- mutual-reachability weight, then the squared
+// Euclidean distance s (bitwise symmetric: (a-b)^2 == (b-a)^2 in the same dimension
+// order), then the ids.  A strict total order on edges, so Boruvka is exact; its primary
+// key is w, so the tree is a minimum spanning tree by weight.  The secondary key s makes
+// weight ties cheap: a lane whose best weight already equals its own core distance (the
+// smallest weight any of its edges can have) needs only candidates with s <= best s, so
+// its search radius shrinks to its nearest tied neighbour instead of the whole core ball.
+struct Best {
+    double w, s;
+    int32_t lo, hi;  // original ids
+};
+__device__ __forceinline__ bool key_less(double w, double s, int32_t lo, int32_t hi, const Best &b) {
+    if (w < b.w) return true;
+    if (w > b.w) return false;
+    if (s < b.s) return true;
+    if (s > b.s) return false;
+    if (lo != b.lo) return lo < b.lo;
+    return hi < b.hi;
+}
+
+// BVH over the Morton-ordered tiles: level 0 = tiles (64 points), level L node i covers
+// level L-1 nodes 8i .. 8i+7.  Node boxes are fixed; node component tags (uniform
+// component id or -1) are rebuilt every round.  slo/shi/stag: the tiles' 16-point groups.
+constexpr int FAN = 8;
+constexpr int MAXLEV = 12;
+struct Bvh {
+    double *lo, *hi;      // [total_nodes][D]
+    int32_t *tag;         // [total_nodes]
+    double *slo, *shi;    // [ntiles * NSG][D]
+    int32_t *stag;        // [ntiles * NSG]
+    int64_t off[MAXLEV + 1];
+    int64_t cnt[MAXLEV];
+    int levels;
+};
+
+template <int D>
+__global__ void bvh_box_kernel(double *__restrict__ lo, double *__restrict__ hi, int64_t child_off, int64_t child_cnt,
+                               int64_t off, int64_t cnt) {
+    HDB_GRID_STRIDE(i, cnt) {
+        int64_t c0 = i * FAN, c1 = min(c0 + FAN, child_cnt);
+        for (int c = 0; c < D; c++) {
+            double l = INFINITY, h = -INFINITY;
+            for (int64_t k = c0; k < c1; k++) {
+                double a = lo[(child_off + k) * D + c], b = hi[(child_off + k) * D + c];
+                l = a < l ? a : l;
+                h = b > h ? b : h;
+            }
+            lo[(off + i) * D + c] = l;
+            hi[(off + i) * D + c] = h;
+        }
+    }
+}
+
+__global__ void bvh_tag_kernel(int32_t *__restrict__ tag, int64_t child_off, int64_t child_cnt, int64_t off,
+                               int64_t cnt) {
+    HDB_GRID_STRIDE(i, cnt) {
+        int64_t c0 = i * FAN, c1 = min(c0 + FAN, child_cnt);
+        int32_t t = tag[child_off + c0];
+        for (int64_t k = c0 + 1; k < c1 && t >= 0; k++)
+            if (tag[child_off + k] != t) t = -1;
+        tag[off + i] = t;
+    }
+}
+
+// lane lower bound (squared) from point x to a box.  Monotone rounding makes it a true
+// lower bound of the computed squared distance of every point in the box (see header).
+template <int D>
+__device__ __forceinline__ double box_lb2(const double (&x)[D], const double *__restrict__ l,
+                                          const double *__restrict__ h) {
+    double lb = 0;
+#pragma unroll
+    for (int c = 0; c < D; c++) {
+        double a = l[c], b = h[c];
+        double g = x[c] < a ? a - x[c] : (x[c] > b ? x[c] - b : 0.0);
+        lb = lb + g * g;
+    }
+    return lb;
+}
+
+// Pushes the children of internal node (lev, idx) that some lane needs, farthest first
+// (so the nearest is popped first), ordered by box-to-box distance from the query tile.
+template <int D, class Needs>
+__device__ __forceinline__ void push_children(const Bvh &bvh, int lev, int64_t idx, const double *qlo,
+                                              const double *qhi, int32_t *stk, int &sp, int lane, Needs needs) {
+    const int64_t c0 = idx * FAN;
+    const int64_t c1 = min(c0 + FAN, bvh.cnt[lev - 1]);
+    double key[FAN];
+    bool ok[FAN];
+#pragma unroll
+    for (int k = 0; k < FAN; k++) {
+        ok[k] = false;
+        key[k] = INFINITY;
+        const int64_t c = c0 + k;
+        if (c < c1) {
+            const int64_t cn = bvh.off[lev - 1] + c;
+            ok[k] = __any(needs(cn));
+            double kk = 0;
+            const double *cl = bvh.lo + cn * D, *ch = bvh.hi + cn * D;
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                double g = qhi[d] < cl[d] ? cl[d] - qhi[d] : (ch[d] < qlo[d] ? qlo[d] - ch[d] : 0.0);
+                kk = kk + g * g;
+            }
+            key[k] = kk;
+        }
+    }
+#pragma unroll 1
+    for (int r = 0; r < FAN; r++) {
+        int sel = -1;
+        double sk = -1.0;
+#pragma unroll
+        for (int k = 0; k < FAN; k++)
+            if (ok[k] && key[k] > sk) {
+                sk = key[k];
+                sel = k;
+            }
+        sel = __builtin_amdgcn_readfirstlane(sel);
+        if (sel < 0) break;
+#pragma unroll
+        for (int k = 0; k < FAN; k++)
+            if (k == sel) ok[k] = false;
+        if (lane == 0) stk[sp] = ((lev - 1) << 26) | (int32_t)(c0 + sel);
+        sp++;
+    }
+}
+
+// Publishes min(v) per component into arr with few atomics: late rounds put most of the
+// n lanes into a handful of components, and one atomicMin per lane on the same address
+// serialises in L2.  A wave whose active lanes share one component reduces first; any
+// lane skips the atomic when the stored value is already <= v.
+__device__ __forceinline__ void publish_min(unsigned long long *arr, int32_t c, unsigned long long v, bool active) {
+    const unsigned long long act = __ballot(active);
+    if (act == 0) return;
+    const int first = __ffsll((long long)act) - 1;
+    const int32_t c0 = __shfl(c, first);
+    if (__all(!active || c == c0)) {
+        unsigned long long m = active ? v : ~0ull;
+        for (int off = 32; off >= 1; off >>= 1) {
+            unsigned long long o = __shfl_xor(m, off);
+            m = o < m ? o : m;
+        }
+        if ((int)(threadIdx.x & 63) == first) {
+            if (m < __hip_atomic_load(&arr[c0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(&arr[c0], m);
+        }
+        return;
+    }
+    if (active && v < __hip_atomic_load(&arr[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(&arr[c], v);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
+                                                          Bvh bvh, unsigned long long *__restrict__ comp_w,
+                                                          double *__restrict__ best_w, double *__restrict__ best_s,
+                                                          int32_t *__restrict__ best_lo, int32_t *__restrict__ best_hi,
+                                                          unsigned long long *__restrict__ stats) {
+    __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
+    const int w = threadIdx.x >> 6;
+    const int64_t t = (int64_t)blockIdx.x * 4 + w;
+    if (t >= ntiles) return;
+    const int lane = threadIdx.x & 63;
+    int32_t *stk = stack_s[w];
+    const int64_t i = t * BT + lane;
+    const bool valid = i < n;
+    unsigned long long n_leaf = 0, nev = 0;
+    double mx[D];
+    double mcore = 0;
+    int32_t mcomp = -3, mid = 0;
+    if (valid) {
+        const Rec<D> r = recs[i];
+#pragma unroll
+        for (int c = 0; c < D; c++) mx[c] = r.x[c];
+        mcore = r.core;
+        mcomp = r.comp;
+        mid = r.id;
+    } else {
+#pragma unroll
+        for (int c = 0; c < D; c++) mx[c] = 0;
+    }
+    Best b{INFINITY, INFINITY, INT32_MAX, INT32_MAX};
+    if (valid && best_w[i] < INFINITY) b = Best{best_w[i], best_s[i], best_lo[i], best_hi[i]};  // seed_kernel
+    double cb2 = INFINITY;  // padded square of the component bound
+    // squared-distance bound from the lane's own best: a candidate can only win with
+    // s <= sb.  b.w == own core: ties need s <= b.s (exact: lb <= s by monotone rounding);
+    // otherwise sqrt(s) <= b.w, i.e. s <= b.w^2 (padded: s > fl(b^2)(1+2^-48) proves
+    // fl(sqrt(s)) > b).
+    auto own_sb = [&]() -> double {
+        if (!(b.w < INFINITY)) return INFINITY;
+        return (b.w <= mcore) ? b.s : (b.w * b.w) * 1.0000000000000036;
+    };
+    double sb = own_sb();
+    auto refresh = [&]() {
+        if (valid) {
+            unsigned long long cw = __hip_atomic_load(&comp_w[mcomp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            double cwd = __longlong_as_double((long long)cw);
+            double c2 = (cwd * cwd) * (1.0 + 1e-12);
+            if (c2 < cb2) cb2 = c2;
+        }
+    };
+    auto bound = [&]() -> double { return sb < cb2 ? sb : cb2; };
+    auto needs_box = [&](const double *lo, const double *hi, int32_t tg) -> bool {
+        if (!valid) return false;
+        if (tg >= 0 && tg == mcomp) return false;
+        const double bd = bound();
+        if (!(bd < INFINITY)) return true;
+        return !(box_lb2<D>(mx, lo, hi) > bd);
+    };
+    auto lane_needs = [&](int64_t node) -> bool { return needs_box(bvh.lo + node * D, bvh.hi + node * D, bvh.tag[node]); };
+    const double *qlo = bvh.lo + t * D, *qhi = bvh.hi + t * D;
+    int sp = 0;
+    if (lane == 0) stk[0] = ((bvh.levels - 1) << 26) | 0;
+    sp = 1;
+    int visits = 0;
+    while (sp > 0) {
+        __builtin_amdgcn_wave_barrier();
+        const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
+        sp--;
+        const int lev = code >> 26;
+        const int64_t idx = code & ((1 << 26) - 1);
+        const int64_t node = bvh.off[lev] + idx;
+        if ((visits++ & 7) == 0) refresh();
+        if (!__any(lane_needs(node))) continue;
+        if (lev > 0) {
+            push_children<D>(bvh, lev, idx, qlo, qhi, stk, sp, lane, lane_needs);
+            continue;
+        }
+        // leaf: tile idx, 4 groups of 16 candidates
+        n_leaf++;
+        bool found = false;
+#pragma unroll 1
+        for (int gi = 0; gi < NSG; gi++) {
+            const int64_t sg = idx * NSG + gi;
+            const bool need = needs_box(bvh.slo + sg * D, bvh.shi + sg * D, bvh.stag[sg]);
+            if (!__any(need)) continue;
+            const int64_t j0 = sg * SG, j1 = min(j0 + SG, n);
+#pragma unroll 4
+            for (int64_t q = j0; q < j1; q++) {
+                const Rec<D> &r = recs[q];  // uniform -> scalar loads
+                double s = sq_diff(mx[0], r.x[0]);
+#pragma unroll
+                for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
+                if (!need || r.comp == mcomp) continue;
+                nev++;  // pair evaluated for a lane that needs it
+                if (!(s <= sb)) continue;  // also drops NaN
+                double mrd = sqrt(s);  // HDBSCANStar.java:162-168 order
+                if (mcore > mrd) mrd = mcore;
+                if (r.core > mrd) mrd = r.core;
+                const int32_t lo = mid < r.id ? mid : r.id;
+                const int32_t hi = mid < r.id ? r.id : mid;
+                if (key_less(mrd, s, lo, hi, b)) {
+                    b = Best{mrd, s, lo, hi};
+                    sb = own_sb();
+                    found = true;
+                }
+            }
+        }
+        if (found) {
+            const double c2 = (b.w * b.w) * (1.0 + 1e-12);
+            if (c2 < cb2) {
+                const unsigned long long bw = (unsigned long long)dbits(b.w);
+                if (bw < __hip_atomic_load(&comp_w[mcomp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    atomicMin(&comp_w[mcomp], bw);
+                cb2 = c2;
+            }
+        }
+    }
+    if (valid) {
+        best_w[i] = b.w;
+        best_s[i] = b.s;
+        best_lo[i] = b.lo;
+        best_hi[i] = b.hi;
+    }
+    publish_min(comp_w, mcomp, dbits(b.w), valid && b.w < INFINITY);
+    if (stats) {
+        for (int off = 32; off >= 1; off >>= 1) nev += __shfl_xor(nev, off);
+        if (lane == 0) {
+            atomicAdd(&stats[0], nev);
+            atomicAdd(&stats[1], n_leaf);
+            atomicAdd(&stats[2], (unsigned long long)visits);
+        }
+    }
+}
+
+// component minimum: comp_w = min w (published during the scan); then min s among the
+// lanes at that weight; then min (lo, hi) among the lanes at (w, s)
+template <int D>
+__global__ void comp_s_kernel(const Rec<D> *__restrict__ recs, int64_t n, const unsigned long long *__restrict__ comp_w,
+                              const double *__restrict__ best_w, const double *__restrict__ best_s,
+                              unsigned long long *__restrict__ comp_s) {
+    HDB_GRID_STRIDE(i, n) {
+        int32_t c = recs[i].comp;
+        double w = best_w[i];
+        if (w < INFINITY && dbits(w) == comp_w[c]) atomicMin(&comp_s[c], dbits(best_s[i]));
+    }
+}
+
+template <int D>
+__global__ void comp_key_kernel(const Rec<D> *__restrict__ recs, int64_t n, const unsigned long long *__restrict__ comp_w,
+                                const unsigned long long *__restrict__ comp_s, const double *__restrict__ best_w,
+                                const double *__restrict__ best_s, const int32_t *__restrict__ best_lo,
+                                const int32_t *__restrict__ best_hi, unsigned long long *__restrict__ comp_key) {
+    HDB_GRID_STRIDE(i, n) {
+        int32_t c = recs[i].comp;
+        double w = best_w[i];
+        if (w < INFINITY && dbits(w) == comp_w[c] && dbits(best_s[i]) == comp_s[c])
+            atomicMin(&comp_key[c], ((unsigned long long)(uint32_t)best_lo[i] << 32) | (uint32_t)best_hi[i]);
+    }
+}
+
+// per component root c: chosen edge -> parent pointer; record edge unless mutual-larger
+template <int D>
+__global__ void hook_kernel(const Rec<D> *__restrict__ recs, int64_t n, const int32_t *__restrict__ inv,
+                            const unsigned long long *__restrict__ comp_w,
+                            const unsigned long long *__restrict__ comp_key, int32_t *__restrict__ parent,
+                            int32_t *__restrict__ out_a, int32_t *__restrict__ out_b, double *__restrict__ out_w,
+                            unsigned long long *__restrict__ n_edges) {
+    HDB_GRID_STRIDE(c, n) {
+        if (recs[c].comp != (int32_t)c) continue;  // not a root
+        unsigned long long k = comp_key[c];
+        if (k == ~0ull) {
+            parent[c] = (int32_t)c;
+            continue;
+        }
+        int32_t lo = (int32_t)(k >> 32), hi = (int32_t)(k & 0xffffffffu);
+        int32_t cl = recs[inv[lo]].comp, ch = recs[inv[hi]].comp;
+        int32_t other = cl == (int32_t)c ? ch : cl;
+        parent[c] = other;
+    }
+}
+
+template <int D>
+__global__ void hook_fix_kernel(const Rec<D> *__restrict__ recs, int64_t n, const unsigned long long *__restrict__ comp_w,
+                                const unsigned long long *__restrict__ comp_key, int32_t *__restrict__ parent,
+                                int32_t *__restrict__ parent2, int32_t *__restrict__ out_a, int32_t *__restrict__ out_b,
+                                double *__restrict__ out_w, unsigned long long *__restrict__ n_edges) {
+    HDB_GRID_STRIDE(c, n) {
+        if (recs[c].comp != (int32_t)c) continue;
+        int32_t p = parent[c];
+        if (p == (int32_t)c) {
+            parent2[c] = p;
+            continue;
+        }
+        bool mutual = parent[p] == (int32_t)c;
+        if (mutual && (int32_t)c < p) {
+            parent2[c] = (int32_t)c;  // smaller id of a mutual pair becomes the root
+        } else {
+            parent2[c] = p;
+        }
+        if (!(mutual && (int32_t)c > p)) {
+            unsigned long long slot = atomicAdd(n_edges, 1ull);
+            unsigned long long k = comp_key[c];
+            out_a[slot] = (int32_t)(k >> 32);
+            out_b[slot] = (int32_t)(k & 0xffffffffu);
+            out_w[slot] = __longlong_as_double((long long)comp_w[c]);
+        }
+    }
+}
+
+// Seeds round r > 0 from round r-1's per-point best edges: an edge whose endpoints are
+// still in different components is a valid candidate for both, so it bounds both
+// components' minimum (published to comp_w) and stays the lane's starting best; otherwise
+// the lane starts empty.  Only valid edges enter comp_w, so the final comp_w is still the
+// true component minimum (its owner lane never prunes it) -- exactness is unchanged.
+template <int D>
+__global__ void seed_kernel(const Rec<D> *__restrict__ recs, int64_t n, const int32_t *__restrict__ inv,
+                            double *__restrict__ best_w, const int32_t *__restrict__ best_lo,
+                            const int32_t *__restrict__ best_hi, unsigned long long *__restrict__ comp_w) {
+    const int64_t stride = (int64_t)blockDim.x * gridDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {  // wave-uniform trip count
+        const int64_t i = base + threadIdx.x;
+        bool act = false;
+        int32_t ca = 0, cb = 0;
+        double w = INFINITY;
+        if (i < n) {
+            w = best_w[i];
+            if (w < INFINITY) {
+                ca = recs[inv[best_lo[i]]].comp;
+                cb = recs[inv[best_hi[i]]].comp;
+                if (ca == cb) best_w[i] = INFINITY;
+                else act = true;
+            }
+        }
+        publish_min(comp_w, ca, dbits(w), act);
+        publish_min(comp_w, cb, dbits(w), act);
+    }
+}
+
+__global__ void fill_inf_kernel(double *__restrict__ p, int64_t n) { HDB_GRID_STRIDE(i, n) p[i] = INFINITY; }
+
+__global__ void jump_kernel(int32_t *__restrict__ parent, int64_t n, int *__restrict__ changed) {
+    HDB_GRID_STRIDE(c, n) {
+        int32_t p = parent[c];
+        if (p < 0) continue;
+        int32_t pp = parent[p];
+        if (pp != p) {
+            parent[c] = pp;
+            *changed = 1;
+        }
+    }
+}
+
+template <int D>
+__global__ void relabel_kernel(Rec<D> *__restrict__ recs, int64_t n, const int32_t *__restrict__ parent) {
+    HDB_GRID_STRIDE(i, n) recs[i].comp = parent[recs[i].comp];
+}
+
+__global__ void mark_nonroot_kernel(int32_t *__restrict__ parent, int64_t n, const int32_t *__restrict__ is_root) {
+    HDB_GRID_STRIDE(c, n) if (!is_root[c]) parent[c] = -1;
+}
+
+template <int D>
+__global__ void roots_kernel(const Rec<D> *__restrict__ recs, int64_t n, int32_t *__restrict__ is_root) {
+    HDB_GRID_STRIDE(c, n) is_root[c] = recs[c].comp == (int32_t)c;
+}
+
+__global__ void edge_idkey_kernel(const int32_t *a, const int32_t *b, int64_t m, uint64_t *k, int32_t *io) {
+    HDB_GRID_STRIDE(i, m) {
+        k[i] = ((uint64_t)(uint32_t)a[i] << 32) | (uint32_t)b[i];
+        io[i] = (int32_t)i;
+    }
+}
+__global__ void edge_wkey_kernel(const int32_t *perm_, const double *ww, int64_t m, uint64_t *k) {
+    HDB_GRID_STRIDE(i, m) k[i] = (uint64_t)__double_as_longlong(ww[perm_[i]]);
+}
+__global__ void edge_out_kernel(const int32_t *perm_, const int32_t *a, const int32_t *b, const double *ww, int64_t m,
+                                int32_t *oa, int32_t *ob, double *ow) {
+    HDB_GRID_STRIDE(i, m) {
+        int32_t p = perm_[i];
+        oa[i] = a[p];
+        ob[i] = b[p];
+        ow[i] = ww[p];
+    }
+}
+
+// ------------------------------------------------------------ K1t: tree kNN
+// A wave owns query tile t (lane = point).  Its own tile is scanned first (it holds the
+// nearest candidates in Morton order, so the K-th bound is tight from the start), then the
+// BVH is walked nearest-first, skipping any node whose box no lane can still improve on.
+// Candidates are wave-uniform (scalar loads); each lane evaluates the exact FP64 squared
+// distance in the reference's order and feeds the register top-K network.
+template <int D, int K>
+__global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
+                                                       Bvh bvh, int excl, double *__restrict__ lists,
+                                                       unsigned long long *__restrict__ stats) {
+    __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
+    const int w = threadIdx.x >> 6;
+    const int64_t t = (int64_t)blockIdx.x * 4 + w;
+    if (t >= ntiles) return;
+    const int lane = threadIdx.x & 63;
+    int32_t *stk = stack_s[w];
+    const int64_t i = t * BT + lane;
+    const bool valid = i < n;
+    double mx[D];
+    int32_t mid = -1;
+    if (valid) {
+        const Rec<D> r = recs[i];
+#pragma unroll
+        for (int c = 0; c < D; c++) mx[c] = r.x[c];
+        mid = r.id;
+    } else {
+#pragma unroll
+        for (int c = 0; c < D; c++) mx[c] = 0;
+    }
+    double buf[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) buf[k] = INFINITY;
+    const int32_t skip_self = excl ? mid : -2;
+    unsigned long long nev = 0, n_leaf = 0, n_node = 0;
+
+    auto needs_box = [&](const double *lo, const double *hi) -> bool {
+        return valid && box_lb2<D>(mx, lo, hi) < buf[K - 1];
+    };
+    auto lane_needs = [&](int64_t node) -> bool { return needs_box(bvh.lo + node * D, bvh.hi + node * D); };
+    auto scan_leaf = [&](int64_t tile, bool own) {
+        n_leaf++;
+#pragma unroll 1
+        for (int gi = 0; gi < NSG; gi++) {
+            const int64_t sg = tile * NSG + gi;
+            if (!own && !__any(needs_box(bvh.slo + sg * D, bvh.shi + sg * D))) continue;
+            const int64_t j0 = sg * SG, j1 = min(j0 + SG, n);
+            nev += (unsigned long long)(j1 - j0);
+#pragma unroll 4
+            for (int64_t q = j0; q < j1; q++) {
+                const Rec<D> &r = recs[q];  // uniform -> scalar loads
+                double s = sq_diff(mx[0], r.x[0]);
+#pragma unroll
+                for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
+                if (r.id == skip_self) s = INFINITY;
+                topk_insert<K>(buf, s);
+            }
+        }
+    };
+    scan_leaf(t, true);  // own tile first: the K-th bound is tight from the start
+    const double *qlo = bvh.lo + t * D, *qhi = bvh.hi + t * D;
+    int sp = 0;
+    if (lane == 0) stk[0] = ((bvh.levels - 1) << 26) | 0;
+    sp = 1;
+    while (sp > 0) {
+        __builtin_amdgcn_wave_barrier();
+        const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
+        sp--;
+        const int lev = code >> 26;
+        const int64_t idx = code & ((1 << 26) - 1);
+        n_node++;
+        if (lev == 0) {
+            if (idx != t && __any(lane_needs(idx))) scan_leaf(idx, false);
+            continue;
+        }
+        push_children<D>(bvh, lev, idx, qlo, qhi, stk, sp, lane, lane_needs);
+    }
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double v = buf[k];
+            lists[(int64_t)mid * K + k] = (v < INFINITY) ? sqrt(v) : JMAX;  // Java keeps Double.MAX_VALUE
+        }
+    }
+    if (stats) {
+        const unsigned long long nvalid = (unsigned long long)__popcll(__ballot(valid));
+        if (lane == 0) {
+            atomicAdd(&stats[0], nev * nvalid);  // (query, candidate) pairs evaluated
+            atomicAdd(&stats[1], n_leaf);
+            atomicAdd(&stats[2], n_node);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- host
+// The index over one partition: Morton-sorted records + BVH (level 0 = 64-point tiles).
+template <int D>
+struct Spatial {
+    int64_t n = 0, ntiles = 0;
+    Rec<D> *recs = nullptr;
+    int32_t *inv = nullptr;  // original id -> sorted position
+    Bvh bvh;
+    // scratch reused by the callers (n entries each)
+    uint64_t *keys = nullptr, *keys2 = nullptr;
+    int32_t *iota = nullptr, *perm = nullptr;
+};
+
+static Bvh bvh_shape(int64_t ntiles) {
+    Bvh bvh;
+    int64_t c = ntiles, tot = 0;
+    bvh.levels = 0;
+    while (true) {
+        if (bvh.levels >= MAXLEV) HDB_THROW(HDB_EINVAL, "spatial index: too many BVH levels");
+        bvh.off[bvh.levels] = tot;
+        bvh.cnt[bvh.levels] = c;
+        tot += c;
+        bvh.levels++;
+        if (c == 1) break;
+        c = ceil_div(c, FAN);
+    }
+    bvh.off[bvh.levels] = tot;
+    return bvh;
+}
+
+// bump allocator over one arena slot: pass 1 sizes (base == nullptr), pass 2 assigns
+struct Carve {
+    char *base = nullptr;
+    size_t off = 0;
+    template <class T>
+    T *take(size_t count) {
+        size_t o = off;
+        off += (sizeof(T) * count + 255) & ~size_t(255);
+        return base ? (T *)(base + o) : nullptr;
+    }
+};
+
+template <int D>
+static void spatial_carve(Carve &cv, Spatial<D> &sp) {
+    const int64_t n = sp.n, nnodes = sp.bvh.off[sp.bvh.levels];
+    sp.bvh.lo = cv.take<double>((size_t)D * nnodes);
+    sp.bvh.hi = cv.take<double>((size_t)D * nnodes);
+    sp.bvh.tag = cv.take<int32_t>(nnodes);
+    sp.bvh.slo = cv.take<double>((size_t)D * sp.ntiles * NSG);
+    sp.bvh.shi = cv.take<double>((size_t)D * sp.ntiles * NSG);
+    sp.bvh.stag = cv.take<int32_t>((size_t)sp.ntiles * NSG);
+    sp.recs = cv.take<Rec<D>>(n);
+    sp.inv = cv.take<int32_t>(n);
+    sp.keys = cv.take<uint64_t>(n);
+    sp.keys2 = cv.take<uint64_t>(n);
+    sp.iota = cv.take<int32_t>(n);
+    sp.perm = cv.take<int32_t>(n);
+}
+
+// Builds the index on ctx->stream.  core nullable (records then carry 0).  `extra` = bytes
+// the caller wants carved after the index in the same arena slot (returned in *extra_ptr).
+template <int D>
+static Spatial<D> build_spatial(hdb_ctx *ctx, const double *X, int64_t n, const double *core, Carve &cv) {
+    if (n > INT32_MAX / 2) HDB_THROW(HDB_EINVAL, "n too large");
+    Spatial<D> sp;
+    sp.n = n;
+    sp.ntiles = ceil_div(n, BT);
+    sp.bvh = bvh_shape(sp.ntiles);
+    spatial_carve<D>(cv, sp);
+    double *blo = cv.take<double>(64), *bhi = cv.take<double>(64);
+    if (!cv.base) return sp;
+    const int g = (int)std::min<int64_t>(ceil_div(n, 256), 4096);
+    hipStream_t st = ctx->stream;
+    hipLaunchKernelGGL(bbox_reduce_kernel, dim3(D), dim3(256), 0, st, X, n, D, blo, bhi);
+    hipLaunchKernelGGL(morton_kernel, dim3(g), dim3(256), 0, st, X, n, D, blo, bhi, sp.keys, sp.iota);
+    {
+        size_t tb = 0;
+        HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, sp.keys, sp.keys2, sp.iota, sp.perm, (int)n, 0, 64, st));
+        void *tmp = arena(ctx, A_SORT, tb);
+        HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, sp.keys, sp.keys2, sp.iota, sp.perm, (int)n, 0, 64, st));
+    }
+    hipLaunchKernelGGL(build_recs_kernel<D>, dim3(g), dim3(256), 0, st, X, core, sp.perm, n, sp.recs, sp.inv);
+    hipLaunchKernelGGL(tile_box_kernel<D>, dim3((unsigned)sp.ntiles), dim3(64), 0, st, sp.recs, n, sp.bvh.lo,
+                       sp.bvh.hi, sp.bvh.slo, sp.bvh.shi);
+    for (int L = 1; L < sp.bvh.levels; L++)
+        hipLaunchKernelGGL(bvh_box_kernel<D>, dim3((unsigned)std::min<int64_t>(ceil_div(sp.bvh.cnt[L], 256), 4096)),
+                           dim3(256), 0, st, sp.bvh.lo, sp.bvh.hi, sp.bvh.off[L - 1], sp.bvh.cnt[L - 1], sp.bvh.off[L],
+                           sp.bvh.cnt[L]);
+    HIP_CHECK(hipGetLastError());
+    return sp;
+}
+
+template <int D>
+static Spatial<D> build_spatial_in(hdb_ctx *ctx, int slot, const double *X, int64_t n, const double *core,
+                                   Carve &cv, size_t extra_bytes, char **extra) {
+    Carve probe;
+    build_spatial<D>(ctx, X, n, core, probe);
+    char *base = (char *)arena(ctx, slot, probe.off + extra_bytes + 256);
+    cv.base = base;
+    cv.off = 0;
+    Spatial<D> sp = build_spatial<D>(ctx, X, n, core, cv);
+    if (extra) *extra = base + ((cv.off + 255) & ~size_t(255));
+    return sp;
+}
+
+// ------------------------------------------------------------------- K1t host
+template <int D, int K>
+static void knn_tree_impl(hdb_ctx *ctx, const double *X, int64_t n, bool excl, double *lists) {
+    Carve cv;
+    char *extra = nullptr;
+    Spatial<D> sp = build_spatial_in<D>(ctx, A_WORK1, X, n, nullptr, cv, 64, &extra);
+    unsigned long long *evals = ctx->count_evals ? (unsigned long long *)extra : nullptr;
+    if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 24, ctx->stream));
+    {
+        KernelTimer t(ctx, "knn_tree");
+        hipLaunchKernelGGL((knn_tree_kernel<D, K>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256), 0, ctx->stream,
+                           sp.recs, n, sp.ntiles, sp.bvh, excl ? 1 : 0, lists, evals);
+        HIP_CHECK(hipGetLastError());
+    }
+    if (evals) {
+        unsigned long long h[3];
+        HIP_CHECK(hipMemcpyAsync(h, evals, 24, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->stats["knn_tree_evals"] = (int64_t)h[0];
+        ctx->stats["knn_tree_leaves"] = (int64_t)h[1];
+        ctx->stats["knn_tree_nodes"] = (int64_t)h[2];
+        ctx->stats["last_evals"] = (int64_t)h[0];
+    }
+}
+
+template <int D>
+static bool knn_tree_k(hdb_ctx *ctx, const double *X, int64_t n, int KC, bool excl, double *lists) {
+    switch (KC) {
+    case 1: knn_tree_impl<D, 1>(ctx, X, n, excl, lists); return true;
+    case 3: knn_tree_impl<D, 3>(ctx, X, n, excl, lists); return true;
+    case 7: knn_tree_impl<D, 7>(ctx, X, n, excl, lists); return true;
+    case 15: knn_tree_impl<D, 15>(ctx, X, n, excl, lists); return true;
+    case 31: knn_tree_impl<D, 31>(ctx, X, n, excl, lists); return true;
+    default: return false;
+    }
+}
+
+bool knn_tree_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC, bool excl, double *lists) {
+    switch (d) {
+    case 1: return knn_tree_k<1>(ctx, X, n, KC, excl, lists);
+    case 2: return knn_tree_k<2>(ctx, X, n, KC, excl, lists);
+    case 3: return knn_tree_k<3>(ctx, X, n, KC, excl, lists);
+    case 4: return knn_tree_k<4>(ctx, X, n, KC, excl, lists);
+    case 8: return knn_tree_k<8>(ctx, X, n, KC, excl, lists);
+    case 16: return knn_tree_k<16>(ctx, X, n, KC, excl, lists);
+    default: return false;
+    }
+}
+
+// ------------------------------------------------------------------- K2b host
+template <int D>
+static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double *core, int32_t *va, int32_t *vb,
+                         double *w) {
+    Carve cv;
+    char *extra = nullptr;
+    // per-round state after the index: comp_w, comp_key (8n each), best_w (8n), best_lo/hi,
+    // parent, parent2, is_root (4n each), counters, edge lists (4n, 4n, 8n)
+    const size_t per = (size_t)n;
+    auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t extra_bytes = 5 * rnd(8 * per) + 5 * rnd(4 * per) + 3 * 256 + 2 * rnd(4 * per) + rnd(8 * per);
+    KernelTimer tt(ctx, "boruvka_total");
+    Spatial<D> sp = build_spatial_in<D>(ctx, A_WORK0, X, n, core, cv, extra_bytes, &extra);
+    Carve ex;
+    ex.base = extra;
+    unsigned long long *comp_w = ex.take<unsigned long long>(per), *comp_key = ex.take<unsigned long long>(per);
+    double *best_w = ex.take<double>(per), *best_s = ex.take<double>(per);
+    unsigned long long *comp_s = ex.take<unsigned long long>(per);
+    int32_t *best_lo = ex.take<int32_t>(per), *best_hi = ex.take<int32_t>(per);
+    int32_t *parent = ex.take<int32_t>(per), *parent2 = ex.take<int32_t>(per), *is_root = ex.take<int32_t>(per);
+    unsigned long long *n_edges = ex.take<unsigned long long>(1);
+    int *changed = ex.take<int>(1);
+    int32_t *ea = ex.take<int32_t>(per), *eb = ex.take<int32_t>(per);
+    double *ew = ex.take<double>(per);
+    unsigned long long *evals = ctx->count_evals ? ex.take<unsigned long long>(3) : nullptr;
+    int64_t tot_evals = 0;
+    Rec<D> *recs = sp.recs;
+    int32_t *inv = sp.inv;
+    Bvh bvh = sp.bvh;
+    const int64_t ntiles = sp.ntiles;
+    int32_t *tcomp = bvh.tag;
+    const int g = (int)std::min<int64_t>(ceil_div(n, 256), 4096);
+    hipStream_t st = ctx->stream;
+    HIP_CHECK(hipMemsetAsync(n_edges, 0, 8, st));
+    hipLaunchKernelGGL(fill_inf_kernel, dim3(g), dim3(256), 0, st, best_w, n);
+    HIP_CHECK(hipGetLastError());
+
+    static const char *round_names[] = {"boruvka_r0", "boruvka_r1", "boruvka_r2", "boruvka_r3", "boruvka_r4",
+                                        "boruvka_r5", "boruvka_r6", "boruvka_r7", "boruvka_r8+"};
+    int64_t have = 0;
+    for (int round = 0; have < n - 1; round++) {
+        if (round > 64) HDB_THROW(HDB_EINVAL, "boruvka did not converge (non-finite distances?)");
+        hipLaunchKernelGGL(tile_comp_kernel<D>, dim3((unsigned)ntiles), dim3(64), 0, st, recs, n, tcomp, bvh.stag);
+        for (int L = 1; L < bvh.levels; L++)
+            hipLaunchKernelGGL(bvh_tag_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(bvh.cnt[L], 256), 4096)),
+                               dim3(256), 0, st, bvh.tag, bvh.off[L - 1], bvh.cnt[L - 1], bvh.off[L], bvh.cnt[L]);
+        HIP_CHECK(hipMemsetAsync(comp_w, 0xff, 8 * n, st));
+        HIP_CHECK(hipMemsetAsync(comp_key, 0xff, 8 * n, st));
+        HIP_CHECK(hipMemsetAsync(comp_s, 0xff, 8 * n, st));
+        if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 24, st));
+        if (round > 0 && ctx->boruvka_seed)
+            hipLaunchKernelGGL(seed_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, inv, best_w, best_lo, best_hi,
+                               comp_w);
+        else if (round > 0)
+            hipLaunchKernelGGL(fill_inf_kernel, dim3(g), dim3(256), 0, st, best_w, n);
+        {
+            KernelTimer ts(ctx, "boruvka_scan");
+            KernelTimer tr(ctx, round_names[round < 8 ? round : 8]);
+            hipLaunchKernelGGL(boruvka_bvh_kernel<D>, dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, st, recs, n,
+                               ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, evals);
+        }
+        if (evals) {
+            unsigned long long h[3];
+            HIP_CHECK(hipMemcpyAsync(h, evals, 24, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            const std::string r = "boruvka_r" + std::to_string(round);
+            ctx->stats[r + "_evals"] = (int64_t)h[0];
+            ctx->stats[r + "_leaves"] = (int64_t)h[1];
+            ctx->stats[r + "_nodes"] = (int64_t)h[2];
+            tot_evals += (int64_t)h[0];
+        }
+        hipLaunchKernelGGL(comp_s_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, comp_w, best_w, best_s, comp_s);
+        hipLaunchKernelGGL(comp_key_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, comp_w, comp_s, best_w, best_s,
+                           best_lo, best_hi, comp_key);
+        hipLaunchKernelGGL(roots_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, is_root);
+        hipLaunchKernelGGL(hook_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, inv, comp_w, comp_key, parent, ea, eb,
+                           ew, n_edges);
+        hipLaunchKernelGGL(hook_fix_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, comp_w, comp_key, parent, parent2,
+                           ea, eb, ew, n_edges);
+        hipLaunchKernelGGL(mark_nonroot_kernel, dim3(g), dim3(256), 0, st, parent2, n, is_root);
+        // pointer jumping to the roots
+        for (int it = 0; it < 64; it++) {
+            int h_changed = 0;
+            HIP_CHECK(hipMemsetAsync(changed, 0, sizeof(int), st));
+            for (int r = 0; r < 4; r++) hipLaunchKernelGGL(jump_kernel, dim3(g), dim3(256), 0, st, parent2, n, changed);
+            HIP_CHECK(hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            if (!h_changed) break;
+        }
+        hipLaunchKernelGGL(relabel_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, parent2);
+        unsigned long long h_ne = 0;
+        HIP_CHECK(hipMemcpyAsync(&h_ne, n_edges, 8, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        HIP_CHECK(hipGetLastError());
+        if ((int64_t)h_ne == have) HDB_THROW(HDB_EINVAL, "boruvka made no progress (non-finite distances?)");
+        have = (int64_t)h_ne;
+    }
+    if (evals) {
+        ctx->stats["boruvka_evals"] = tot_evals;
+        ctx->stats["last_evals"] = tot_evals;
+    }
+    // sort edges by (w, lo, hi): stable sort by (lo,hi) then stable by w
+    {
+        int64_t ne = n - 1;
+        if (ne > 0) {
+            uint64_t *k1 = sp.keys, *k2 = sp.keys2;
+            int32_t *p1 = sp.iota, *p2 = sp.perm;
+            hipLaunchKernelGGL(edge_idkey_kernel, dim3(g), dim3(256), 0, st, ea, eb, ne, k1, p1);
+            size_t tb = 0;
+            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1, k2, p1, p2, (int)ne, 0, 64, st));
+            void *tmp = arena(ctx, A_SORT, tb);
+            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k1, k2, p1, p2, (int)ne, 0, 64, st));
+            hipLaunchKernelGGL(edge_wkey_kernel, dim3(g), dim3(256), 0, st, p2, ew, ne, k1);
+            // stable sort by w (non-negative doubles: bit order == numeric order)
+            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1, k2, p2, p1, (int)ne, 0, 64, st));
+            tmp = arena(ctx, A_SORT, tb);
+            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k1, k2, p2, p1, (int)ne, 0, 64, st));
+            hipLaunchKernelGGL(edge_out_kernel, dim3(g), dim3(256), 0, st, p1, ea, eb, ew, ne, va, vb, w);
+            HIP_CHECK(hipGetLastError());
+        }
+    }
+}
+
+void boruvka_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const double *core, int metric, int32_t *va,
+                    int32_t *vb, double *w) {
+    if (metric != HDB_METRIC_EUCLIDEAN) HDB_THROW(HDB_EINVAL, "boruvka: euclidean metric only");
+    if (n <= 1) return;
+    switch (d) {
+    case 1: boruvka_impl<1>(ctx, X, n, core, va, vb, w); break;
+    case 2: boruvka_impl<2>(ctx, X, n, core, va, vb, w); break;
+    case 3: boruvka_impl<3>(ctx, X, n, core, va, vb, w); break;
+    case 4: boruvka_impl<4>(ctx, X, n, core, va, vb, w); break;
+    case 8: boruvka_impl<8>(ctx, X, n, core, va, vb, w); break;
+    case 16: boruvka_impl<16>(ctx, X, n, core, va, vb, w); break;
+    default: HDB_THROW(HDB_EINVAL, "boruvka: d must be one of 1,2,3,4,8,16");
+    }
+}
+
+}  // namespace hdb

@@ -66,9 +66,17 @@ int hdb_ctx_set_timing(hdb_ctx *ctx, int enable);
  * since the last reset, then resets that accumulator when reset != 0. */
 int hdb_ctx_kernel_time(hdb_ctx *ctx, const char *name, double *ms_total, int64_t *launches, int reset);
 int hdb_ctx_synchronize(hdb_ctx *ctx);
-/* Tuning/diagnostic switches: "knn_fp32_screen" (default 1) = K1 screens pairs in FP32
- * with a rigorous bound before the exact FP64 test (results identical either way). */
+/* Tuning/diagnostic switches (results are identical under every setting):
+ *   "knn_fp32_screen" (default 1): K1 screens pairs in FP32 with a rigorous bound before the
+ *                                  exact FP64 test;
+ *   "knn_tree"        (default 1): euclidean k-NN lists of partitions with n >= "knn_tree_min_n"
+ *                                  (default 8192) and d in {1,2,3,4,8,16} use K1t, the
+ *                                  box-pruned traversal of the Morton/BVH index, instead of
+ *                                  the all-pairs K1;
+ *   "count_evals"     (default 0): K1t counts the pairs it evaluates (read "last_evals"). */
 int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value);
+/* Diagnostic counters: "last_evals" = pair evaluations of the last K1t call (count_evals on). */
+int hdb_ctx_get_stat(hdb_ctx *ctx, const char *name, int64_t *value);
 const char *hdb_last_error(void);
 int hdb_version(void);
 

@@ -1,0 +1,135 @@
+"""K1t (box-pruned k-NN over the Morton/BVH index, csrc/spatial.hip) parity: the lists and
+all three core semantics must equal the oracle and the all-pairs K1 bit for bit, for every
+d the index supports, every minPts bucket, duplicates, ties, non-finite values and ragged
+tile counts.  The tree only skips pairs that provably fail the strict '<' insertion test
+(HDBSCANStar.java:89), so any difference is a bug.
+"""
+import contextlib
+
+import numpy as np
+import pytest
+
+from conftest import blobs, load_skin
+
+pytestmark = pytest.mark.gpu
+
+
+def eq(a, b):
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    if a.shape != b.shape:
+        return False
+    na, nb = np.isnan(a), np.isnan(b)
+    if not np.array_equal(na, nb):
+        return False
+    return np.array_equal(np.where(na, 0.0, a).view(np.uint64), np.where(nb, 0.0, b).view(np.uint64))
+
+
+@contextlib.contextmanager
+def options(ctx, **kw):
+    defaults = {"knn_tree": 1, "knn_tree_min_n": 8192, "knn_fp32_screen": 1, "count_evals": 0}
+    try:
+        for k, v in kw.items():
+            ctx.set_option(k, v)
+        yield
+    finally:
+        for k in kw:
+            ctx.set_option(k, defaults[k])
+
+
+@pytest.fixture(scope="module")
+def ctx(pkg):
+    c = pkg.Context(0)
+    c.use_torch_stream()  # device tensors below are produced/consumed on torch's stream
+    return c
+
+
+@pytest.fixture(scope="module")
+def star(pkg, ctx):
+    return pkg.HDBSCANStar(ctx)
+
+
+def tree_cores(ctx, star, X, mp, sem):
+    with options(ctx, knn_tree=1, knn_tree_min_n=0):
+        return star.calculateCoreDistances(X, mp, None, sem)
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 4, 8, 16])
+@pytest.mark.parametrize("min_pts", [2, 4, 8, 16, 32])
+def test_tree_cores_vs_oracle(ctx, star, oracle, d, min_pts):
+    X = blobs(2500, d, 6, 7 * d + min_pts)
+    for sem in range(3):
+        assert eq(tree_cores(ctx, star, X, min_pts, sem), oracle.core_distances(X, min_pts, semantics=sem)), sem
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 63, 64, 65, 511, 513, 4097])
+def test_tree_ragged_sizes(ctx, star, oracle, n):
+    X = blobs(n, 3, 3, n)
+    for sem in range(3):
+        assert eq(tree_cores(ctx, star, X, 4, sem), oracle.core_distances(X, 4, semantics=sem)), (n, sem)
+
+
+def test_tree_duplicates_skin(ctx, star, oracle):
+    X = load_skin(20000)  # integer RGB, max multiplicity in the hundreds: zero-distance ties
+    for sem in range(3):
+        assert eq(tree_cores(ctx, star, X, 4, sem), oracle.core_distances(X, 4, semantics=sem)), sem
+
+
+def test_tree_lists_equal_dense(ctx, star):
+    X = blobs(60000, 3, 12, 21)
+    for k in (1, 3, 7, 15, 31):
+        with options(ctx, knn_tree=1, knn_tree_min_n=0):
+            a = star.knn(X, k, None, exclSelf=True)
+        with options(ctx, knn_tree=0):
+            b = star.knn(X, k, None, exclSelf=True)
+        assert eq(a, b), k
+
+
+@pytest.mark.parametrize("d", [2, 8, 16])
+def test_tree_equals_dense_mid_size(ctx, star, d):
+    X = blobs(30000, d, 30, 100 + d, spread=20.0)
+    for sem in range(3):
+        a = tree_cores(ctx, star, X, 8, sem)
+        with options(ctx, knn_tree=0):
+            b = star.calculateCoreDistances(X, 8, None, sem)
+        assert eq(a, b), sem
+
+
+def test_tree_uniform_and_scales(ctx, star, oracle):
+    rng = np.random.default_rng(3)
+    for scale in (1e-9, 1.0, 1e8, 1e150):
+        X = rng.uniform(-1, 1, size=(3000, 3)) * scale
+        X[10:20] = X[9]
+        for sem in range(3):
+            assert eq(tree_cores(ctx, star, X, 5, sem), oracle.core_distances(X, 5, semantics=sem)), (scale, sem)
+
+
+def test_tree_nonfinite(ctx, star, oracle):
+    X = blobs(2000, 3, 3, 5)
+    X[7, 1] = np.nan
+    X[100, 0] = np.inf
+    X[101, 2] = -np.inf
+    for sem in range(3):
+        assert eq(tree_cores(ctx, star, X, 4, sem), oracle.core_distances(X, 4, semantics=sem)), sem
+
+
+def test_tree_prunes(ctx, star):
+    """Diagnostic counter: at 200k clustered points the tree evaluates a tiny fraction of n^2."""
+    X = blobs(200_000, 3, 20, 1)
+    with options(ctx, knn_tree=1, knn_tree_min_n=0, count_evals=1):
+        star.calculateCoreDistances(X, 4, None, 2)
+        ev = ctx.get_stat("last_evals")
+    assert 0 < ev < 0.01 * 200_000 ** 2
+
+
+def test_tree_full_size_rows(star):
+    """1M x 3 (config 2) through the default path (tree): exact per-row check on a sample."""
+    import torch
+    X = blobs(1_000_000, 3, 20, 1)
+    got = star.calculateCoreDistances(torch.from_numpy(X).cuda(), 4, None, 2).cpu().numpy()
+    rng = np.random.default_rng(6)
+    for r in rng.choice(X.shape[0], 24, replace=False):
+        s = (X[r, 0] - X[:, 0]) * (X[r, 0] - X[:, 0])
+        s = s + (X[r, 1] - X[:, 1]) * (X[r, 1] - X[:, 1])
+        s = s + (X[r, 2] - X[:, 2]) * (X[r, 2] - X[:, 2])
+        s[r] = np.inf
+        assert got[r] == np.sqrt(np.partition(s, 2)[:3].max()), r
