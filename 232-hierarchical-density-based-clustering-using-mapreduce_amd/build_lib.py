@@ -16,7 +16,8 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.environ.get("HDBMI_OUT") or os.path.join(HERE, "lib")
 LIB = os.path.join(OUT, "libhdbmi.so")
 SOURCES = ["context.cpp", "capi.cpp", "local_model.cpp", "knn.hip", "nearest.hip", "prim.hip",
-           "bubbles.hip", "merge.hip", "spatial.hip"]
+           "bubbles.hip", "merge.hip", "spatial.hip"] + [f"knn_d{d}.hip" for d in (1, 2, 3, 4, 5, 6, 8, 16)]
+HEADERS = ["common.hpp", "internal.hpp", "knn_impl.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # -ffp-contract=off: the reference (Java) never fuses a*b+c; bit-exact parity needs the same.
@@ -31,7 +32,7 @@ def _obj(src: str) -> str:
 
 def _stamp(src: str) -> str:
     h = hashlib.sha1()
-    for f in [src, "common.hpp", "internal.hpp"]:
+    for f in [src, *HEADERS]:
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
     with open(os.path.join(HERE, "..", "include", "hdbmi.h"), "rb") as fh:
@@ -60,7 +61,7 @@ def _compile(src: str, force: bool) -> str:
 
 def build(jobs: int | None = None, force: bool = False) -> str:
     os.makedirs(OUT, exist_ok=True)
-    jobs = jobs or min(8, os.cpu_count() or 4)
+    jobs = jobs or min(16, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
     newest = max(os.path.getmtime(o) for o in objs)

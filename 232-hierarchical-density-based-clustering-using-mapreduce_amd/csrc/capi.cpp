@@ -233,15 +233,7 @@ int hdb_mst_boruvka(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const d
         int32_t *dva = s.out(va, ne), *dvb = s.out(vb, ne);
         double *dw = s.out(w, ne);
         boruvka_device(ctx, dX, n, d, dc, metric, dva, dvb, dw);
-        if (self_edges) {
-            // self edges (v, v, core[v]) after the n-1 tree edges
-            std::vector<int32_t> iv(n);
-            for (int64_t i = 0; i < n; i++) iv[i] = (int32_t)i;
-            HIP_CHECK(hipMemcpyAsync(dva + (n - 1), iv.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
-            HIP_CHECK(hipMemcpyAsync(dvb + (n - 1), iv.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
-            HIP_CHECK(hipMemcpyAsync(dw + (n - 1), dc, sizeof(double) * n, hipMemcpyDeviceToDevice, ctx->stream));
-            HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        }
+        if (self_edges) self_edges_device(ctx, dc, n, dva + (n - 1), dvb + (n - 1), dw + (n - 1));
         s.finish();
     });
 }

@@ -48,30 +48,65 @@ struct Rec {
 __device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
 
 // ---------------------------------------------------------------- morton
-__global__ void bbox_reduce_kernel(const double *__restrict__ X, int64_t n, int d, double *__restrict__ lo,
-                                   double *__restrict__ hi) {
-    // one block per dimension (d <= 64)
-    const int c = blockIdx.x;
-    __shared__ double sl[256], sh[256];
-    double l = INFINITY, h = -INFINITY;
-    for (int64_t i = threadIdx.x; i < n; i += 256) {
-        double v = X[i * d + c];
-        l = fmin(l, v);
-        h = fmax(h, v);
+// bounding box of X: per-block partial min/max over rows (fmin/fmax ignore NaN), then one
+// block folds the partials
+constexpr int BBOX_BLOCKS = 1024;
+template <int D>
+__global__ __launch_bounds__(256) void bbox_partial_kernel(const double *__restrict__ X, int64_t n,
+                                                           double *__restrict__ part) {
+    double l[D], h[D];
+#pragma unroll
+    for (int c = 0; c < D; c++) {
+        l[c] = INFINITY;
+        h[c] = -INFINITY;
     }
-    sl[threadIdx.x] = l;
-    sh[threadIdx.x] = h;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-            sl[threadIdx.x] = fmin(sl[threadIdx.x], sl[threadIdx.x + s]);
-            sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + s]);
+    HDB_GRID_STRIDE(i, n) {
+#pragma unroll
+        for (int c = 0; c < D; c++) {
+            const double v = X[i * D + c];
+            l[c] = fmin(l[c], v);
+            h[c] = fmax(h[c], v);
         }
-        __syncthreads();
+    }
+    __shared__ double sl[4][D], sh[4][D];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < D; c++) {
+        for (int off = 32; off >= 1; off >>= 1) {
+            l[c] = fmin(l[c], __shfl_xor(l[c], off));
+            h[c] = fmax(h[c], __shfl_xor(h[c], off));
+        }
+        if (lane == 0) {
+            sl[w][c] = l[c];
+            sh[w][c] = h[c];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < D) {
+        const int c = threadIdx.x;
+        double a = fmin(fmin(sl[0][c], sl[1][c]), fmin(sl[2][c], sl[3][c]));
+        double b = fmax(fmax(sh[0][c], sh[1][c]), fmax(sh[2][c], sh[3][c]));
+        part[(int64_t)blockIdx.x * 2 * D + c] = a;
+        part[(int64_t)blockIdx.x * 2 * D + D + c] = b;
+    }
+}
+template <int D>
+__global__ void bbox_final_kernel(const double *__restrict__ part, int nb, double *__restrict__ lo,
+                                  double *__restrict__ hi) {
+    // one wave per dimension
+    const int c = blockIdx.x;
+    double l = INFINITY, h = -INFINITY;
+    for (int k = threadIdx.x; k < nb; k += 64) {
+        l = fmin(l, part[(int64_t)k * 2 * D + c]);
+        h = fmax(h, part[(int64_t)k * 2 * D + D + c]);
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        l = fmin(l, __shfl_xor(l, off));
+        h = fmax(h, __shfl_xor(h, off));
     }
     if (threadIdx.x == 0) {
-        lo[c] = sl[0];
-        hi[c] = sh[0];
+        lo[c] = l;
+        hi[c] = h;
     }
 }
 
@@ -762,10 +797,13 @@ static Spatial<D> build_spatial(hdb_ctx *ctx, const double *X, int64_t n, const 
     sp.bvh = bvh_shape(sp.ntiles);
     spatial_carve<D>(cv, sp);
     double *blo = cv.take<double>(64), *bhi = cv.take<double>(64);
+    double *bpart = cv.take<double>((size_t)BBOX_BLOCKS * 2 * D);
     if (!cv.base) return sp;
     const int g = (int)std::min<int64_t>(ceil_div(n, 256), 4096);
     hipStream_t st = ctx->stream;
-    hipLaunchKernelGGL(bbox_reduce_kernel, dim3(D), dim3(256), 0, st, X, n, D, blo, bhi);
+    const int nbb = (int)std::min<int64_t>(BBOX_BLOCKS, ceil_div(n, 256));
+    hipLaunchKernelGGL(bbox_partial_kernel<D>, dim3(nbb), dim3(256), 0, st, X, n, bpart);
+    hipLaunchKernelGGL(bbox_final_kernel<D>, dim3(D), dim3(64), 0, st, bpart, nbb, blo, bhi);
     hipLaunchKernelGGL(morton_kernel, dim3(g), dim3(256), 0, st, X, n, D, blo, bhi, sp.keys, sp.iota);
     {
         size_t tb = 0;
@@ -967,6 +1005,22 @@ static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double 
             HIP_CHECK(hipGetLastError());
         }
     }
+}
+
+__global__ void self_edges_kernel(const double *__restrict__ core, int64_t n, int32_t *__restrict__ va,
+                                  int32_t *__restrict__ vb, double *__restrict__ w) {
+    HDB_GRID_STRIDE(i, n) {
+        va[i] = (int32_t)i;
+        vb[i] = (int32_t)i;
+        w[i] = core[i];
+    }
+}
+
+void self_edges_device(hdb_ctx *ctx, const double *core, int64_t n, int32_t *va, int32_t *vb, double *w) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(self_edges_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 256), 4096)), dim3(256), 0,
+                       ctx->stream, core, n, va, vb, w);
+    HIP_CHECK(hipGetLastError());
 }
 
 void boruvka_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const double *core, int metric, int32_t *va,
