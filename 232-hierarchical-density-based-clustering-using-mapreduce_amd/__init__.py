@@ -11,6 +11,7 @@ from ._capi import (BUBBLE_CF, BUBBLE_COMBINESTEP, CORE_EXCL_SELF, CORE_INCL_SEL
                     NullPointerException, lib)
 from .databubbles import (CombineStep, FirstStep, HdbscanDataBubbles, LocalModelReduceByKey,
                           bubble_stats, nearest_sample, sort_edges_desc)
+from .driver import MRHDBSCANStar
 from .hdbscanstar import (CosineSimilarity, DistanceCalculator, EuclideanDistance, HDBSCANStar,
                           ManhattanDistance, PearsonCorrelation, SupremumDistance, UndirectedGraph,
                           distance_rows)

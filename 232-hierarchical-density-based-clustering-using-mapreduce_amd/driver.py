@@ -1,0 +1,250 @@
+"""MR-HDBSCAN* iteration driver over the HIP operators -- the stand-in for the reference's
+Spark driver (main/Main.java:103-347) used by the end-to-end tests and benchmarks.
+
+In production the Java/Spark driver stays in place and calls the operators through JNI
+(INTEGRATION.md); this module runs the same loop without Spark, device-resident: the points
+stay in HBM for the whole run, every level's work is batched over all subsets of the level,
+and only per-subset bookkeeping (a few integers per subset, one label per bubble) touches
+the host.  Semantics follow Main.java with the deterministic deviations of SURVEY.md
+Appendix A.2 (D1-D10, listed in oracle/mr_driver.py, which restates the same loop on the CPU
+oracle for the parity tests):
+
+  level loop (Main.java:107)   subsets grouped by key, ascending (D5)
+  leaves  (FirstStep.java:104-120)  subsets <= processing_units (or forced, D9): cumulative
+          core distances + Prim with self edges over the rows in ascending global id, one
+          batched launch for all leaves <= LEAF_PRIM_MAX points; larger forced leaves use
+          the same cores + Boruvka (exact weights; topology differs from Prim only on ties)
+  big subsets: D2 samples -> keyed nearest sample (FirstStep.java:74-85, D3) -> bulk
+          CombineStep (D5 fold order) -> per subset LocalModelReduceByKey (D4) -> partition
+          induction (Main.java:272-289, including the in-place relabel) -> LabelClassification
+  merge   UnionFindReducer + SortMST: stable descending sort of the iteration-major edge list
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import _capi as A
+from .hdbscanstar import metric_of
+
+LEAF_PRIM_MAX = 4096  # leaves up to this size run the exact reference Prim (batched)
+
+
+def sample_ids(n_key: int, k: float, samples_per_subset, seed: int, iteration: int, key: int):
+    """D2: positions (into the subset's rows, ascending global id) of the subset's samples,
+    ascending; size ceil(k * n) (sampleByKeyExact, Main.java:141) or an explicit count."""
+    m = samples_per_subset if samples_per_subset else int(math.ceil(k * n_key))
+    m = max(1, min(n_key, m))
+    rng = np.random.Generator(np.random.PCG64([seed, iteration, key]))
+    return np.sort(rng.choice(n_key, size=m, replace=False)).astype(np.int64)
+
+
+class MRHDBSCANStar:
+    """Main.main's MR-HDBSCAN* loop (with data bubbles) on one device."""
+
+    def __init__(self, minPts=4, minClSize=4, processing_units=50, k=0.2, samples_per_subset=None,
+                 seed=20210101, distanceFunction=None, all_inter_edges=True, max_levels=64, ctx=None,
+                 device=0):
+        self.minPts = minPts
+        self.minClSize = minClSize
+        self.processing_units = processing_units
+        self.k = k
+        self.samples_per_subset = samples_per_subset
+        self.seed = seed
+        self.metric = metric_of(distanceFunction)
+        self.all_inter_edges = all_inter_edges
+        self.max_levels = max_levels
+        self.device = device
+        self.ctx = ctx
+
+    # ------------------------------------------------------------------ helpers
+    def _c(self):
+        if self.ctx is None:
+            self.ctx = A.Context.get(self.device)
+        self.ctx.use_torch_stream()
+        return self.ctx
+
+    def _leaves(self, X, rows_list, keys):
+        """FirstStep leaf branch for every leaf subset of the level; returns edge tuples in
+        key order."""
+        import torch
+        out = []
+        c = self._c()
+        small = [(k, r) for k, r in zip(keys, rows_list) if r.shape[0] <= LEAF_PRIM_MAX]
+        if small:
+            rows = torch.cat([r for _, r in small])
+            sizes = np.array([r.shape[0] for _, r in small], np.int64)
+            offs = np.zeros(len(small) + 1, np.int64)
+            offs[1:] = np.cumsum(sizes)
+            Xl = X.index_select(0, rows).contiguous()
+            ids = rows.to(torch.int32)
+            ne = int(np.sum(2 * sizes - 1))
+            core = torch.empty(rows.shape[0], dtype=torch.float64, device=X.device)
+            va = torch.empty(ne, dtype=torch.int32, device=X.device)
+            vb = torch.empty_like(va)
+            w = torch.empty(ne, dtype=torch.float64, device=X.device)
+            A.check(A.lib().hdb_leaf_msts(c.h, Xl.data_ptr(), offs.ctypes.data, len(small), X.shape[1],
+                                          ids.data_ptr(), self.minPts, self.metric, core.data_ptr(), va.data_ptr(),
+                                          vb.data_ptr(), w.data_ptr()), "FirstStep.leaf")
+            eo = np.zeros(len(small) + 1, np.int64)
+            eo[1:] = np.cumsum(2 * sizes - 1)
+            by_key = {k: (va[eo[i]:eo[i + 1]], vb[eo[i]:eo[i + 1]], w[eo[i]:eo[i + 1]])
+                      for i, (k, _) in enumerate(small)}
+        else:
+            by_key = {}
+        for k, r in zip(keys, rows_list):
+            if k in by_key:
+                out.append(by_key[k])
+                continue
+            # large forced leaf (D9): cumulative cores + Boruvka (exact weights)
+            Xl = X.index_select(0, r).contiguous()
+            n = r.shape[0]
+            core = torch.empty(n, dtype=torch.float64, device=X.device)
+            A.check(A.lib().hdb_core_distances(c.h, Xl.data_ptr(), n, X.shape[1], self.minPts, self.metric,
+                                               A.CORE_INCL_SELF_CUMULATIVE, core.data_ptr()), "leaf cores")
+            ne = 2 * n - 1
+            va = torch.empty(ne, dtype=torch.int32, device=X.device)
+            vb = torch.empty_like(va)
+            w = torch.empty(ne, dtype=torch.float64, device=X.device)
+            A.check(A.lib().hdb_mst_boruvka(c.h, Xl.data_ptr(), n, X.shape[1], core.data_ptr(), self.metric, 1,
+                                            va.data_ptr(), vb.data_ptr(), w.data_ptr()), "leaf boruvka")
+            g = r.to(torch.int32)
+            out.append((g[va.long()], g[vb.long()], w))
+        return out
+
+    # --------------------------------------------------------------------- run
+    def run(self, X):
+        """X: n x d float64 (numpy or torch).  Returns dict(edges=(va, vb, w) merged,
+        levels=[...], leaf_of=subset key that processed each point, iterations)."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        X = torch.as_tensor(X, dtype=torch.float64).to(dev).contiguous()
+        n, d = X.shape
+        c = self._c()
+        key_of = torch.zeros(n, dtype=torch.int64, device=dev)
+        alive = torch.arange(n, dtype=torch.int64, device=dev)  # ids in the current _unprocessed_ file
+        forced = set()
+        leaf_of = torch.full((n,), -1, dtype=torch.int64, device=dev)
+        edge_lists, levels = [], []
+        iteration, processed, next_id = 0, 0, 2  # Main.java:103-105
+        while processed < n:
+            # group the alive records by (key, global id) -- D5
+            order = torch.argsort(key_of[alive] * (n + 1) + alive)
+            alive = alive[order]
+            akeys = key_of[alive]
+            ukeys, counts = torch.unique_consecutive(akeys, return_counts=True)
+            ukeys, counts = ukeys.cpu().numpy(), counts.cpu().numpy()
+            starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+            leaf_k, leaf_rows, big = [], [], []
+            for kk, s0, cnt in zip(ukeys.tolist(), starts.tolist(), counts.tolist()):  # Main.java:133-138
+                rows = alive[s0:s0 + cnt]
+                if cnt <= self.processing_units or kk in forced or iteration >= self.max_levels:
+                    leaf_k.append(kk)
+                    leaf_rows.append(rows)
+                    processed += cnt
+                else:
+                    big.append((kk, s0, cnt))
+            level = dict(iteration=iteration, leaves={k: int(r.shape[0]) for k, r in zip(leaf_k, leaf_rows)},
+                         big={k: cnt for k, _, cnt in big}, labels={}, new_keys={})
+            if leaf_k:
+                edge_lists.extend(self._leaves(X, leaf_rows, leaf_k))
+                for kk, r in zip(leaf_k, leaf_rows):
+                    leaf_of[r] = kk
+            iteration += 1
+            if processed >= n:
+                levels.append(level)
+                break
+            # ---- big subsets: samples (D2), keyed nearest sample (D3), bubbles
+            brows = torch.cat([alive[s0:s0 + cnt] for _, s0, cnt in big])
+            bkey_local = torch.cat([torch.full((cnt,), i, dtype=torch.int32, device=dev)
+                                    for i, (_, _, cnt) in enumerate(big)])
+            s_gid, s_key, s_off = [], [], [0]
+            for i, (kk, s0, cnt) in enumerate(big):
+                sp = torch.from_numpy(sample_ids(cnt, self.k, self.samples_per_subset, self.seed, iteration - 1, kk))
+                s_gid.append(alive[s0:s0 + cnt][sp.to(dev)])
+                s_key.append(torch.full((sp.shape[0],), i, dtype=torch.int32, device=dev))
+                s_off.append(s_off[-1] + sp.shape[0])
+            s_gid = torch.cat(s_gid)
+            s_key = torch.cat(s_key)
+            Xb = X.index_select(0, brows).contiguous()
+            S = X.index_select(0, s_gid).contiguous()
+            nearest = torch.empty(brows.shape[0], dtype=torch.int32, device=dev)
+            A.check(A.lib().hdb_nearest_sample(c.h, Xb.data_ptr(), Xb.shape[0], S.data_ptr(), S.shape[0], d,
+                                               self.metric, bkey_local.data_ptr(), s_key.data_ptr(),
+                                               nearest.data_ptr(), None), "FirstStep.nearest")
+            # nearest is the list position in S (keyed: within the point's own subset)
+            nb = S.shape[0]
+            ls = torch.empty((nb, d), dtype=torch.float64, device=dev)
+            ss, rep = torch.empty_like(ls), torch.empty_like(ls)
+            info = torch.empty((nb, 3), dtype=torch.float64, device=dev)
+            A.check(A.lib().hdb_bubble_stats(c.h, Xb.data_ptr(), Xb.shape[0], d, nearest.data_ptr(), nb,
+                                             A.BUBBLE_COMBINESTEP, ls.data_ptr(), ss.data_ptr(), rep.data_ptr(),
+                                             info.data_ptr()), "CombineStep")
+            rep_h, info_h = rep.cpu().numpy(), info.cpu().numpy()
+            s_gid_h = s_gid.cpu().numpy()
+            new_key_of_bubble = np.full(nb, -2, np.int64)
+            inter = []
+            for i, (kk, s0, cnt) in enumerate(big):
+                a, b = s_off[i], s_off[i + 1]
+                nonempty = np.nonzero(info_h[a:b, 2] > 0)[0]  # D4
+                labels = None
+                if nonempty.shape[0] >= 2:
+                    try:
+                        labels, iedges = self._local_model(rep_h[a:b][nonempty], info_h[a:b][nonempty])
+                    except A.HdbError as e:  # D10
+                        level.setdefault("model_errors", {})[kk] = e.code
+                        labels = None
+                    else:
+                        iva, ivb, iw = iedges
+                        if iw.shape[0]:
+                            gid = s_gid_h[a:b][nonempty].astype(np.int32)
+                            if self.all_inter_edges:  # D7
+                                inter.append((gid[iva], gid[ivb], iw))
+                            else:
+                                inter.append((iva[:1], ivb[:1], iw[:1]))
+                if labels is None:
+                    labels = np.full(nonempty.shape[0], 2, np.int32)
+                level["labels"][kk] = labels.copy()
+                for cl in sorted(set(labels.tolist())):  # Main.java:272-289 (in-place relabel)
+                    labels[labels == cl] = next_id
+                    next_id += 1
+                nk = sorted(set(labels.tolist()))
+                level["new_keys"][kk] = nk
+                if len(nk) == 1:
+                    forced.add(nk[0])  # D9
+                new_key_of_bubble[a + nonempty] = labels
+            # LabelClassification.java:21-37 (bubble of the point -> relabelled label)
+            tbl = torch.from_numpy(new_key_of_bubble).to(dev)
+            key_of[brows] = tbl[nearest.long()]
+            for va, vb, w in inter:
+                edge_lists.append((torch.from_numpy(np.ascontiguousarray(va, np.int32)).to(dev),
+                                   torch.from_numpy(np.ascontiguousarray(vb, np.int32)).to(dev),
+                                   torch.from_numpy(np.ascontiguousarray(w, np.float64)).to(dev)))
+            alive = brows
+            levels.append(level)
+        # UnionFindReducer + SortMST: stable descending sort of the concatenation
+        va = torch.cat([e[0] for e in edge_lists]) if edge_lists else torch.zeros(0, dtype=torch.int32, device=dev)
+        vb = torch.cat([e[1] for e in edge_lists]) if edge_lists else torch.zeros(0, dtype=torch.int32, device=dev)
+        w = torch.cat([e[2] for e in edge_lists]) if edge_lists else torch.zeros(0, dtype=torch.float64, device=dev)
+        if w.shape[0]:
+            A.check(A.lib().hdb_sort_edges_desc(c.h, va.data_ptr(), vb.data_ptr(), w.data_ptr(), w.shape[0]),
+                    "SortMST")
+        return dict(edges=(va, vb, w), levels=levels, leaf_of=leaf_of, iterations=iteration)
+
+    def _local_model(self, rep, info):
+        """LocalModelReduceByKey.java:88-104 body (D4 ids) -> (labels, inter-cluster edges)."""
+        rep = np.ascontiguousarray(rep, np.float64)
+        info = np.ascontiguousarray(info, np.float64)
+        b, d = rep.shape
+        ne = 2 * b - 1
+        labels = np.zeros(b, np.int32)
+        mva, mvb, mw = np.zeros(ne, np.int32), np.zeros(ne, np.int32), np.zeros(ne)
+        iva, ivb, iw = np.zeros(ne, np.int32), np.zeros(ne, np.int32), np.zeros(ne)
+        nic = np.zeros(1, np.int64)
+        c = self._c()
+        A.check(A.lib().hdb_local_model(c.h, A.ptr(rep), A.ptr(info), b, d, self.minPts, self.minClSize, self.metric,
+                                        A.ptr(labels), A.ptr(mva), A.ptr(mvb), A.ptr(mw), A.ptr(iva), A.ptr(ivb),
+                                        A.ptr(iw), A.ptr(nic)), "LocalModelReduceByKey")
+        k = int(nic[0])
+        return labels, (iva[:k], ivb[:k], iw[:k])

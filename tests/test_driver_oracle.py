@@ -1,0 +1,48 @@
+"""CPU: the oracle's restatement of the MR-HDBSCAN* loop (oracle/mr_driver.py) terminates,
+is deterministic, and with D7 (all inter-cluster edges) returns a spanning tree of the data
+plus one self edge per point."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import scipy.sparse.csgraph as cg
+
+from conftest import blobs, load_iris, load_skin
+
+
+def spanning(X, r):
+    va, vb, w = r["edges"]
+    n = X.shape[0]
+    m = va != vb
+    assert m.sum() == n - 1 and (~m).sum() == n
+    G = sp.coo_matrix((np.ones(m.sum()), (va[m], vb[m])), shape=(n, n))
+    assert cg.connected_components(G, directed=False)[0] == 1
+    assert np.all(np.diff(w) <= 0)  # SortMST: descending
+    assert np.all(r["leaf_of"] >= 0)
+
+
+@pytest.mark.parametrize("name,pu,k", [("iris", 50, 0.2), ("blobs", 300, 0.1), ("skin", 300, 0.1)])
+def test_oracle_driver_spanning_and_deterministic(name, pu, k):
+    from oracle import mr_driver as M
+    X = {"iris": load_iris, "blobs": lambda: blobs(3000, 3, 6, 1), "skin": lambda: load_skin(3000)}[name]()
+    a = M.run(X, processing_units=pu, k=k)
+    b = M.run(X, processing_units=pu, k=k)
+    spanning(X, a)
+    for x, y in zip(a["edges"], b["edges"]):
+        assert np.array_equal(x, y)
+
+
+def test_oracle_driver_skin_d10():
+    """Skin subsets make the reference's cluster tree throw (Clusters.java:45-46); D10 turns
+    the subset into a forced leaf instead of ending the run."""
+    from oracle import mr_driver as M
+    r = M.run(load_skin(3000), processing_units=300, k=0.1)
+    assert r["levels"][0]["model_errors"] == {0: -12}
+
+
+def test_sample_ids_shared_with_product():
+    """D2's sampler is the same function in the product driver and the oracle driver."""
+    import importlib
+    from oracle import mr_driver as M
+    drv = importlib.import_module("232-hierarchical-density-based-clustering-using-mapreduce_amd.driver")
+    for n, k, s in [(100, 0.2, None), (5000, 0.01, None), (3000, 0.5, 64)]:
+        assert np.array_equal(M.sample_ids(n, k, s, 7, 2, 5), drv.sample_ids(n, k, s, 7, 2, 5))

@@ -1,0 +1,55 @@
+"""End-to-end MR-HDBSCAN* (Main.java:103-347 with D1-D10) on the device: the product driver
+(driver.py, HIP operators) against the CPU oracle's restatement of the same loop
+(oracle/mr_driver.py).  Every level's subsets, bubble labels, induced keys, the leaf that
+processed each point and the merged edge list must match exactly."""
+import numpy as np
+import pytest
+
+from conftest import blobs, load_iris, load_skin
+
+pytestmark = pytest.mark.gpu
+
+
+def run_both(pkg, X, **kw):
+    from oracle import mr_driver as M
+    ref = M.run(X, **kw)
+    got = pkg.MRHDBSCANStar(minPts=kw.get("min_pts", 4), minClSize=kw.get("min_cl_size", 4),
+                            processing_units=kw["processing_units"], k=kw.get("k", 0.2),
+                            samples_per_subset=kw.get("samples_per_subset"),
+                            all_inter_edges=kw.get("all_inter_edges", True)).run(X)
+    return ref, got
+
+
+def check(ref, got):
+    assert got["iterations"] == ref["iterations"]
+    assert len(got["levels"]) == len(ref["levels"])
+    for a, b in zip(got["levels"], ref["levels"]):
+        assert a["leaves"] == b["leaves"] and a["big"] == b["big"]
+        assert a["new_keys"] == b["new_keys"]
+        assert a.get("model_errors") == b.get("model_errors")
+        for k in b["labels"]:
+            assert np.array_equal(a["labels"][k], b["labels"][k]), k
+    assert np.array_equal(got["leaf_of"].cpu().numpy(), ref["leaf_of"])
+    for x, y in zip(got["edges"], ref["edges"]):
+        assert np.array_equal(x.cpu().numpy(), y)
+
+
+@pytest.mark.parametrize("name,pu,k", [("iris", 50, 0.2), ("blobs3k", 300, 0.1), ("blobs3k", 1000, 0.05),
+                                       ("skin3k", 300, 0.1), ("blobs8k_d8", 1500, 0.02)])
+def test_driver_matches_oracle(pkg, name, pu, k):
+    X = {"iris": lambda: load_iris(), "blobs3k": lambda: blobs(3000, 3, 6, 1),
+         "skin3k": lambda: load_skin(3000), "blobs8k_d8": lambda: blobs(8000, 8, 10, 2, spread=30.0)}[name]()
+    ref, got = run_both(pkg, X, processing_units=pu, k=k)
+    check(ref, got)
+
+
+def test_driver_literal_first_inter_edge(pkg):
+    X = blobs(3000, 3, 6, 1)
+    ref, got = run_both(pkg, X, processing_units=300, k=0.1, all_inter_edges=False)
+    check(ref, got)
+
+
+def test_driver_samples_per_subset(pkg):
+    X = blobs(6000, 2, 8, 4)
+    ref, got = run_both(pkg, X, processing_units=800, samples_per_subset=200)
+    check(ref, got)
