@@ -14,6 +14,6 @@ from .databubbles import (CombineStep, FirstStep, HdbscanDataBubbles, LocalModel
 from .driver import MRHDBSCANStar
 from .hdbscanstar import (CosineSimilarity, DistanceCalculator, EuclideanDistance, HDBSCANStar,
                           ManhattanDistance, PearsonCorrelation, SupremumDistance, UndirectedGraph,
-                          distance_rows)
+                          distance_rows, flat_labels)
 
 __all__ = [n for n in dir() if not n.startswith("_")]

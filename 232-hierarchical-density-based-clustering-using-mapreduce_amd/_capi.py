@@ -98,6 +98,7 @@ def lib():
             "hdb_local_model": [vp, dp, dp, i64, i32, i32, i32, i32, ip, ip, ip, dp, ip, ip, dp, lp],
             "hdb_quicksort_edges": [ip, ip, dp, i64],
             "hdb_sort_edges_desc": [vp, ip, ip, dp, i64],
+            "hdb_flat_labels": [vp, ip, ip, dp, i64, i64, i32, ip, lp],
         }
         for name, args in sig.items():
             f = getattr(L, name)
@@ -116,7 +117,7 @@ EXPORTED = ["hdb_ctx_create", "hdb_ctx_destroy", "hdb_ctx_set_stream", "hdb_ctx_
             "hdb_distance_rows", "hdb_core_distances", "hdb_knn", "hdb_prim_mst", "hdb_prim_mst_batched",
             "hdb_leaf_msts", "hdb_mst_boruvka", "hdb_nearest_sample", "hdb_bubble_stats",
             "hdb_bubble_core_distances", "hdb_bubble_prim_mst", "hdb_local_model", "hdb_quicksort_edges",
-            "hdb_sort_edges_desc"]
+            "hdb_sort_edges_desc", "hdb_flat_labels"]
 
 
 def check(rc: int, what: str):

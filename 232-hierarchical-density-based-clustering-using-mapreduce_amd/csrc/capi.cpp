@@ -385,4 +385,44 @@ int hdb_sort_edges_desc(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64
     });
 }
 
+int hdb_flat_labels(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, const double *w, int64_t ne, int64_t n,
+                    int32_t min_cl_size, int32_t *labels, int64_t *n_clusters) {
+    if (!ctx) {  // host-only use (all pointers in host memory): no device needed
+        try {
+            if (ne < 0 || n < 0 || (ne > 0 && (!va || !vb || !w)) || (n > 0 && !labels))
+                HDB_THROW(HDB_EINVAL, "bad arguments");
+            return flat_labels_host(va, vb, w, ne, n, min_cl_size, labels, n_clusters);
+        } catch (const Error &e) {
+            set_error(e.msg);
+            return e.code;
+        } catch (const std::bad_alloc &) {
+            set_error("host allocation failed");
+            return HDB_ENOMEM;
+        }
+    }
+    return guarded(ctx, [&] {
+        if (ne < 0 || n < 0 || (ne > 0 && (!va || !vb || !w)) || (n > 0 && !labels)) HDB_THROW(HDB_EINVAL, "bad arguments");
+        // host algorithm: bring device inputs over once
+        auto host = [&](const void *p, size_t bytes, std::vector<char> &buf) -> const void * {
+            if (!p || !is_device_ptr(p)) return p;
+            buf.resize(bytes);
+            HIP_CHECK(hipMemcpyAsync(buf.data(), p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+            return buf.data();
+        };
+        std::vector<char> ba, bb, bw;
+        const int32_t *ha = (const int32_t *)host(va, sizeof(int32_t) * (size_t)ne, ba);
+        const int32_t *hb = (const int32_t *)host(vb, sizeof(int32_t) * (size_t)ne, bb);
+        const double *hw = (const double *)host(w, sizeof(double) * (size_t)ne, bw);
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        const bool dev_out = labels && is_device_ptr(labels);
+        std::vector<int32_t> hl(dev_out ? (size_t)n : 0);
+        int32_t *out = dev_out ? hl.data() : labels;
+        flat_labels_host(ha, hb, hw, ne, n, min_cl_size, out, n_clusters);
+        if (dev_out) {
+            HIP_CHECK(hipMemcpyAsync(labels, hl.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+            HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        }
+    });
+}
+
 }  // extern "C"

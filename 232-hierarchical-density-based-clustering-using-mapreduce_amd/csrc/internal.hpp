@@ -40,6 +40,8 @@ void boruvka_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const doubl
 // host logic (local_model.cpp)
 int bubble_core_epilogue(const double *rep, const int32_t *nB, const double *eB, const double *nnB, int64_t b, int d,
                          int min_pts, int metric, const double *knn, const int32_t *log, double *core);
+int flat_labels_host(const int32_t *va, const int32_t *vb, const double *w, int64_t ne, int64_t n, int32_t mcs,
+                     int32_t *labels, int64_t *n_clusters);
 int quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne);
 int local_model_host(const double *rep, const double *eB, const double *nnB, const int32_t *nB, int64_t b, int d,
                      int32_t min_cl_size, int metric, int32_t *mva, int32_t *mvb, double *mw, int32_t *labels,

@@ -45,7 +45,7 @@ class MRHDBSCANStar:
 
     def __init__(self, minPts=4, minClSize=4, processing_units=50, k=0.2, samples_per_subset=None,
                  seed=20210101, distanceFunction=None, all_inter_edges=True, max_levels=64, ctx=None,
-                 device=0):
+                 device=0, flat_labels=True):
         self.minPts = minPts
         self.minClSize = minClSize
         self.processing_units = processing_units
@@ -57,6 +57,7 @@ class MRHDBSCANStar:
         self.max_levels = max_levels
         self.device = device
         self.ctx = ctx
+        self.flat_labels = flat_labels
 
     # ------------------------------------------------------------------ helpers
     def _c(self):
@@ -230,7 +231,17 @@ class MRHDBSCANStar:
         if w.shape[0]:
             A.check(A.lib().hdb_sort_edges_desc(c.h, va.data_ptr(), vb.data_ptr(), w.data_ptr(), w.shape[0]),
                     "SortMST")
-        return dict(edges=(va, vb, w), levels=levels, leaf_of=leaf_of, iterations=iteration)
+        out = dict(edges=(va, vb, w), levels=levels, leaf_of=leaf_of, iterations=iteration)
+        if self.flat_labels and self.all_inter_edges:
+            # D6: the global hierarchy + flat partition over the merged MST (replaces the
+            # System.exit(1) of Main.java:408); D7 makes the merged edges a spanning tree
+            labels = torch.empty(n, dtype=torch.int32, device=dev)
+            k = np.zeros(1, np.int64)
+            A.check(A.lib().hdb_flat_labels(c.h, va.data_ptr(), vb.data_ptr(), w.data_ptr(), w.shape[0], n,
+                                            self.minClSize, labels.data_ptr(), k.ctypes.data), "flat labels")
+            out["labels"] = labels
+            out["n_clusters"] = int(k[0])
+        return out
 
     def _local_model(self, rep, info):
         """LocalModelReduceByKey.java:88-104 body (D4 ids) -> (labels, inter-cluster edges)."""

@@ -172,6 +172,17 @@ int hdb_quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne);
  * sort).  The cross-GPU all-gather feeding it runs over RCCL in the host layer. */
 int hdb_sort_edges_desc(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne);
 
+/* ------------------------------------------------ global flat labels (§8(f) #1)
+ * The step the reference never completes (Main.java:351-408): HDBSCAN* hierarchy over the
+ * merged MST and its flat FOSC / excess-of-mass partition -- HDBSCANStar.java:208-625
+ * (computeHierarchyAndClusterTree, propagateTree, findProminentClusters; commented out in the
+ * reference) without constraints, canonical tie rules (DESIGN.md "flat labels").
+ * va/vb/w: the merged edge list (self edges ignored; the rest must form a spanning tree of
+ * the n points).  labels: n ints, 1..K by ascending smallest member id, 0 = noise.
+ * min_cl_size >= 2.  ctx may be NULL when every pointer is host memory (pure host algorithm). */
+int hdb_flat_labels(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, const double *w, int64_t ne, int64_t n,
+                    int32_t min_cl_size, int32_t *labels, int64_t *n_clusters);
+
 #ifdef __cplusplus
 }
 #endif

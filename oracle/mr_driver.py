@@ -132,4 +132,8 @@ def run(X, min_pts=4, min_cl_size=4, processing_units=50, k=0.2, samples_per_sub
         alive = new_alive
         levels.append(level)
     va, vb, w = O.merge_edges(edge_lists)                  # UnionFindReducer + SortMST
-    return dict(edges=(va, vb, w), levels=levels, leaf_of=leaf_of, iterations=iteration)
+    out = dict(edges=(va, vb, w), levels=levels, leaf_of=leaf_of, iterations=iteration)
+    if all_inter_edges:                                    # D6: global flat labels
+        from .flat_labels import flat_labels
+        out["labels"], out["n_clusters"] = flat_labels(n, va, vb, w, min_cl_size)
+    return out

@@ -32,6 +32,9 @@ def check(ref, got):
     assert np.array_equal(got["leaf_of"].cpu().numpy(), ref["leaf_of"])
     for x, y in zip(got["edges"], ref["edges"]):
         assert np.array_equal(x.cpu().numpy(), y)
+    if "labels" in ref:  # D6 global flat labels
+        assert got["n_clusters"] == ref["n_clusters"]
+        assert np.array_equal(got["labels"].cpu().numpy(), ref["labels"])
 
 
 @pytest.mark.parametrize("name,pu,k", [("iris", 50, 0.2), ("blobs3k", 300, 0.1), ("blobs3k", 1000, 0.05),
@@ -53,3 +56,17 @@ def test_driver_samples_per_subset(pkg):
     X = blobs(6000, 2, 8, 4)
     ref, got = run_both(pkg, X, processing_units=800, samples_per_subset=200)
     check(ref, got)
+
+
+def test_flat_labels_device_inputs(pkg, oracle):
+    """hdb_flat_labels on HBM-resident edges (staged once) equals the oracle."""
+    import torch
+    from oracle.flat_labels import flat_labels
+    X = blobs(20000, 3, 12, 3)
+    core = oracle.core_distances(X, 4, semantics=oracle.EXCL_SELF)
+    star = pkg.HDBSCANStar()
+    mst = star.constructMSTBoruvka(torch.from_numpy(X).cuda(), torch.from_numpy(core).cuda(), True)
+    va, vb, w = mst.getVerticeA(), mst.getVericeB(), mst.getEges()
+    lab, k = pkg.flat_labels(va, vb, w, X.shape[0], 10)
+    ref, kr = flat_labels(X.shape[0], va.cpu().numpy(), vb.cpu().numpy(), w.cpu().numpy(), 10)
+    assert k == kr and np.array_equal(lab.cpu().numpy(), ref)
