@@ -4,6 +4,8 @@
 #include <algorithm>
 #include <vector>
 
+#include <chrono>
+
 #include "internal.hpp"
 
 using namespace hdb;
@@ -346,8 +348,14 @@ int hdb_local_model(hdb_ctx *ctx, const double *rep, const double *info, int64_t
             nB[i] = (int32_t)info_h[i * 3 + 2];
             ids[i] = (int32_t)i;  // D4: vertex id == position
         }
+        using clk = std::chrono::steady_clock;
+        auto us = [](clk::time_point a, clk::time_point b) {
+            return (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
+        };
+        auto t0 = clk::now();
         std::vector<double> core;
         bubble_core_impl(ctx, rep_h.data(), nB.data(), eB.data(), nnB.data(), b, d, min_pts, metric, core);
+        auto t1 = clk::now();
         const int64_t ne = 2 * b - 1;
         std::vector<int32_t> mva(ne), mvb(ne);
         std::vector<double> mw(ne);
@@ -356,12 +364,20 @@ int hdb_local_model(hdb_ctx *ctx, const double *rep, const double *info, int64_t
             prim_common(ctx, rep_h.data(), offs, 1, d, core.data(), ids.data(), eB.data(), nnB.data(), metric, 1,
                         mva.data(), mvb.data(), mw.data());
         }
+        auto t2 = clk::now();
+        g_lm_us[0] = g_lm_us[1] = g_lm_us[2] = 0;
         std::vector<int32_t> lab(b);
         std::vector<int32_t> iva(ne), ivb(ne);
         std::vector<double> iw(ne);
         int64_t nic = 0;
         int rc = local_model_host(rep_h.data(), eB.data(), nnB.data(), nB.data(), b, d, min_cl_size, metric, mva.data(),
                                   mvb.data(), mw.data(), lab.data(), iva.data(), ivb.data(), iw.data(), &nic);
+        ctx->stats["lm_core_us"] += us(t0, t1);
+        ctx->stats["lm_prim_us"] += us(t1, t2);
+        ctx->stats["lm_quicksort_us"] += g_lm_us[0];
+        ctx->stats["lm_tree_us"] += g_lm_us[1];
+        ctx->stats["lm_fosc_us"] += g_lm_us[2];
+        ctx->stats["lm_calls"] += 1;
         if (rc) HDB_THROW(rc, "local model raised a reference exception");
         std::copy(lab.begin(), lab.end(), labels);
         if (mst_va) std::copy(mva.begin(), mva.end(), mst_va);

@@ -9,12 +9,13 @@
 //   * findInterClusterEdges (:506-527).
 // Host C++ built with -ffp-contract=off so the few host distance evaluations match Java.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <numeric>
 #include <vector>
 
-#include "common.hpp"
+#include "internal.hpp"
 
 namespace hdb {
 
@@ -204,6 +205,8 @@ static int construct_cluster_tree(int64_t b, const int32_t *ea, const int32_t *e
         root.numPoints = (int32_t)all;
         clusters.push_back(root);
     }
+    std::vector<int32_t> idx_of(2, -1);  // cluster label -> index in `clusters`
+    idx_of[1] = 0;
     std::vector<uint32_t> stamp(b, 0);
     uint32_t gen = 0;
     std::vector<int32_t> queue;
@@ -278,12 +281,12 @@ static int construct_cluster_tree(int64_t b, const int32_t *ea, const int32_t *e
                     newc.push_back(std::move(c));
                 } else {
                     for (int32_t v : queue) label[v] = 0;
-                    for (auto &c : clusters)
-                        if (c.label == parentLabel && c.death == JMAX) {
-                            int rc = detach(c, (int32_t)countMembers, cw);
-                            if (rc) return rc;
-                            break;
-                        }
+                    // first live cluster with that label (labels are unique in `clusters`)
+                    const int32_t ci = parentLabel < (int32_t)idx_of.size() ? idx_of[parentLabel] : -1;
+                    if (ci >= 0 && clusters[ci].death == JMAX) {
+                        int rc = detach(clusters[ci], (int32_t)countMembers, cw);
+                        if (rc) return rc;
+                    }
                 }
             }
             if (newc.size() >= 2) {
@@ -291,13 +294,14 @@ static int construct_cluster_tree(int64_t b, const int32_t *ea, const int32_t *e
                     c.label = nextLabel;
                     for (int32_t v : c.members) label[v] = nextLabel;
                     nextLabel++;
-                    for (auto &pc : clusters)
-                        if (pc.label == c.parent && pc.death == JMAX) {
-                            pc.hasChildren = true;
-                            int rc = detach(pc, c.numPoints, c.birth);
-                            if (rc) return rc;
-                            break;
-                        }
+                    const int32_t pi = c.parent < (int32_t)idx_of.size() ? idx_of[c.parent] : -1;
+                    if (pi >= 0 && clusters[pi].death == JMAX) {
+                        clusters[pi].hasChildren = true;
+                        int rc = detach(clusters[pi], c.numPoints, c.birth);
+                        if (rc) return rc;
+                    }
+                    if ((int32_t)idx_of.size() <= c.label) idx_of.resize((size_t)c.label + 1, -1);
+                    idx_of[c.label] = (int32_t)clusters.size();
                     clusters.push_back(std::move(c));
                 }
             }
@@ -338,15 +342,19 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
         }
     };
     (void)find_key;
-    for (auto *par : tree) {
+    // for par in tree: for ch in tree: par.label == ch.parent -> adj[par] += ch (tree order);
+    // labels are unique, so one pass over the children builds the same lists
+    std::vector<Cl *> by_label(maxlab + 2, nullptr);
+    for (auto *c : tree) by_label[c->label] = c;
+    for (auto *par : tree)
         if (!par->hasChildren) put(par->label);
-        for (auto *ch : tree) {
-            if (par->label == ch->parent) {
-                put(par->label);
-                Rec r{{par->stability, (double)ch->label, ch->stability, 1.0, (double)par->parent}};
-                get(par->label)->push_back(r);
-            }
-        }
+    for (auto *ch : tree) {
+        if (ch->parent < 0 || ch->parent > maxlab) continue;
+        Cl *par = by_label[ch->parent];
+        if (!par) continue;
+        put(par->label);
+        Rec r{{par->stability, (double)ch->label, ch->stability, 1.0, (double)par->parent}};
+        get(par->label)->push_back(r);
     }
     // Collections.sort by birth level (stable)
     std::vector<Cl *> sorted = tree;
@@ -354,7 +362,8 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
     for (int64_t o = 0; o < b; o++) flat[o] = 0;
     std::vector<char> sol(maxlab + 2, 0);
     for (auto *c : sorted) sol[c->label] = 1;
-    std::vector<char> vis(maxlab + 2, 0);
+    std::vector<uint32_t> vis(maxlab + 2, 0);  // generation stamps (one BFS per record)
+    uint32_t vgen = 0;
     std::vector<int32_t> q;
     for (auto *c : sorted) {
         const int32_t key = c->label;
@@ -365,10 +374,13 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
             for (auto &r : *A) childStab += r.v[2];
             if (childStab <= (*A)[0].v[0]) {
                 for (auto &r : *A) {
-                    std::fill(vis.begin(), vis.end(), 0);
+                    if (++vgen == 0) {
+                        std::fill(vis.begin(), vis.end(), 0);
+                        vgen = 1;
+                    }
                     int32_t rootV = (int32_t)r.v[1];
                     q.clear();
-                    vis[rootV] = 1;
+                    vis[rootV] = vgen;
                     q.push_back(rootV);
                     r.v[3] = 0.0;
                     sol[rootV] = 0;
@@ -379,9 +391,9 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
                             for (auto &rr : *Av) {
                                 sol[v] = 0;
                                 int32_t cc = (int32_t)rr.v[1];
-                                if (!vis[cc]) {
+                                if (vis[cc] != vgen) {
                                     q.push_back(cc);
-                                    vis[cc] = 1;
+                                    vis[cc] = vgen;
                                 }
                             }
                     }
@@ -423,16 +435,28 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
     return HDB_OK;
 }
 
+thread_local int64_t g_lm_us[3];
+
 int local_model_host(const double *rep, const double *eB, const double *nnB, const int32_t *nB, int64_t b, int d,
                      int32_t min_cl_size, int metric, int32_t *mva, int32_t *mvb, double *mw, int32_t *labels,
                      int32_t *ic_va, int32_t *ic_vb, double *ic_w, int64_t *n_ic) {
+    using clk = std::chrono::steady_clock;
+    auto us = [](clk::time_point a, clk::time_point b) {
+        return (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
+    };
     const int64_t ne = 2 * b - 1;
+    auto t0 = clk::now();
     int rc = quicksort_edges(mva, mvb, mw, ne);
     if (rc) return rc;
+    auto t1 = clk::now();
     std::vector<Cl> cl;
     rc = construct_cluster_tree(b, mva, mvb, mw, ne, min_cl_size, nB, cl);
+    auto t2 = clk::now();
+    g_lm_us[0] += us(t0, t1);
+    g_lm_us[1] += us(t1, t2);
     if (rc) return rc;
     rc = find_prominent(cl, rep, eB, nnB, b, d, metric, labels);
+    g_lm_us[2] += us(t2, clk::now());
     if (rc) return rc;
     int64_t k = 0;
     for (int64_t i = 0; i < ne; i++)

@@ -45,7 +45,7 @@ class MRHDBSCANStar:
 
     def __init__(self, minPts=4, minClSize=4, processing_units=50, k=0.2, samples_per_subset=None,
                  seed=20210101, distanceFunction=None, all_inter_edges=True, max_levels=64, ctx=None,
-                 device=0, flat_labels=True):
+                 device=0, flat_labels=True, profile=False):
         self.minPts = minPts
         self.minClSize = minClSize
         self.processing_units = processing_units
@@ -58,6 +58,20 @@ class MRHDBSCANStar:
         self.device = device
         self.ctx = ctx
         self.flat_labels = flat_labels
+        self.profile = profile       # phase wall times (synchronising) in self.timings
+        self.timings = {}
+        self._t0 = None
+
+    def _mark(self, phase):
+        if not self.profile:
+            return
+        import time
+        import torch
+        torch.cuda.synchronize(self.device)
+        now = time.perf_counter()
+        if self._t0 is not None and phase:
+            self.timings[phase] = self.timings.get(phase, 0.0) + (now - self._t0)
+        self._t0 = now
 
     # ------------------------------------------------------------------ helpers
     def _c(self):
@@ -123,6 +137,9 @@ class MRHDBSCANStar:
         X = torch.as_tensor(X, dtype=torch.float64).to(dev).contiguous()
         n, d = X.shape
         c = self._c()
+        self.timings = {}
+        self._t0 = None
+        self._mark(None)
         key_of = torch.zeros(n, dtype=torch.int64, device=dev)
         alive = torch.arange(n, dtype=torch.int64, device=dev)  # ids in the current _unprocessed_ file
         forced = set()
@@ -149,7 +166,9 @@ class MRHDBSCANStar:
             level = dict(iteration=iteration, leaves={k: int(r.shape[0]) for k, r in zip(leaf_k, leaf_rows)},
                          big={k: cnt for k, _, cnt in big}, labels={}, new_keys={})
             if leaf_k:
+                self._mark("bookkeeping")
                 edge_lists.extend(self._leaves(X, leaf_rows, leaf_k))
+                self._mark("leaves")
                 for kk, r in zip(leaf_k, leaf_rows):
                     leaf_of[r] = kk
             iteration += 1
@@ -174,6 +193,7 @@ class MRHDBSCANStar:
             A.check(A.lib().hdb_nearest_sample(c.h, Xb.data_ptr(), Xb.shape[0], S.data_ptr(), S.shape[0], d,
                                                self.metric, bkey_local.data_ptr(), s_key.data_ptr(),
                                                nearest.data_ptr(), None), "FirstStep.nearest")
+            self._mark("nearest_sample")
             # nearest is the list position in S (keyed: within the point's own subset)
             nb = S.shape[0]
             ls = torch.empty((nb, d), dtype=torch.float64, device=dev)
@@ -183,6 +203,7 @@ class MRHDBSCANStar:
                                              A.BUBBLE_COMBINESTEP, ls.data_ptr(), ss.data_ptr(), rep.data_ptr(),
                                              info.data_ptr()), "CombineStep")
             rep_h, info_h = rep.cpu().numpy(), info.cpu().numpy()
+            self._mark("bubbles")
             s_gid_h = s_gid.cpu().numpy()
             new_key_of_bubble = np.full(nb, -2, np.int64)
             inter = []
@@ -216,6 +237,7 @@ class MRHDBSCANStar:
                     forced.add(nk[0])  # D9
                 new_key_of_bubble[a + nonempty] = labels
             # LabelClassification.java:21-37 (bubble of the point -> relabelled label)
+            self._mark("local_models")
             tbl = torch.from_numpy(new_key_of_bubble).to(dev)
             key_of[brows] = tbl[nearest.long()]
             for va, vb, w in inter:
@@ -224,6 +246,7 @@ class MRHDBSCANStar:
                                    torch.from_numpy(np.ascontiguousarray(w, np.float64)).to(dev)))
             alive = brows
             levels.append(level)
+        self._mark("bookkeeping")
         # UnionFindReducer + SortMST: stable descending sort of the concatenation
         va = torch.cat([e[0] for e in edge_lists]) if edge_lists else torch.zeros(0, dtype=torch.int32, device=dev)
         vb = torch.cat([e[1] for e in edge_lists]) if edge_lists else torch.zeros(0, dtype=torch.int32, device=dev)
@@ -232,6 +255,7 @@ class MRHDBSCANStar:
             A.check(A.lib().hdb_sort_edges_desc(c.h, va.data_ptr(), vb.data_ptr(), w.data_ptr(), w.shape[0]),
                     "SortMST")
         out = dict(edges=(va, vb, w), levels=levels, leaf_of=leaf_of, iterations=iteration)
+        self._mark("merge")
         if self.flat_labels and self.all_inter_edges:
             # D6: the global hierarchy + flat partition over the merged MST (replaces the
             # System.exit(1) of Main.java:408); D7 makes the merged edges a spanning tree
@@ -241,6 +265,7 @@ class MRHDBSCANStar:
                                             self.minClSize, labels.data_ptr(), k.ctypes.data), "flat labels")
             out["labels"] = labels
             out["n_clusters"] = int(k[0])
+            self._mark("flat_labels")
         return out
 
     def _local_model(self, rep, info):
