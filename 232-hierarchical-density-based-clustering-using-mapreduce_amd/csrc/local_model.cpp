@@ -164,7 +164,32 @@ struct Cl {
     double birth, death = JMAX, stability = 0;
     int32_t numPoints;
     bool hasChildren = false;
-    std::vector<int32_t> members;  // TreeSet order
+    std::vector<int32_t> members;  // TreeSet order (BFS path)
+    int32_t node = -1;             // fast path: members = leaves of this dendrogram node
+};
+
+// Component dendrogram of the (quicksorted) MST edge list, built bottom-up: the component a
+// vertex belongs to after the top-down walk has removed edges [j, ne) is the union-find
+// state after edges [0, j).  Leaves 0..b-1 are the vertices; node k >= b merges l, r.
+struct Dendro {
+    int64_t b = 0;
+    std::vector<int32_t> l, r;     // children of internal node b + k
+    std::vector<int64_t> sum_nb;   // sum of nB over the node's vertices
+    std::vector<int32_t> size;     // vertex count
+    template <class F>
+    void leaves(int32_t node, std::vector<int32_t> &stk, F &&f) const {
+        stk.assign(1, node);
+        while (!stk.empty()) {
+            int32_t x = stk.back();
+            stk.pop_back();
+            if (x < b) {
+                f(x);
+                continue;
+            }
+            stk.push_back(r[x - b]);
+            stk.push_back(l[x - b]);
+        }
+    }
 };
 
 static int detach(Cl &c, int32_t numPoints, double level) {  // Clusters.java:39-47
@@ -180,7 +205,204 @@ static uint32_t jhash(int32_t k) {
     return h ^ (h >> 16);
 }
 
-static int construct_cluster_tree(int64_t b, const int32_t *ea, const int32_t *eb, const double *ew, int64_t ne,
+
+// Fast equivalent of construct_cluster_tree_bfs below: the same top-down control flow
+// (tie runs from the heaviest, HashMap order of affected labels, TreeSet order of affected
+// vertices, one "BFS" per affected vertex including the reference's re-processing of an
+// already-explored component), but a component is read off the dendrogram instead of
+// being re-explored: Sigma nB and the vertex set come from the pre-run union-find node.
+// Labels are kept per component group (every live component owns one group; on a split all
+// pieces but the largest move to fresh groups -- small-to-large, O(b log b) moves), so
+// labelling a component noise or a new cluster is O(1).  Returns 1 (not an error) when the
+// edges are not a forest plus self edges; the caller then runs the BFS version.
+static int construct_cluster_tree_fast(int64_t b, const int32_t *ea, const int32_t *eb, const double *ew, int64_t ne,
+                                       int32_t mcl, const int32_t *nB, std::vector<Cl> &clusters, Dendro &D) {
+    for (int64_t i = 0; i < ne; i++) {
+        if (ea[i] < 0 || ea[i] >= b || eb[i] < 0 || eb[i] >= b) return HDB_EREF_OOB;
+        if (ew[i] != ew[i]) return HDB_EINVAL;  // NaN level: the reference's walk never advances
+    }
+    // ---- bottom-up: pre-run component node of every edge endpoint
+    D.b = b;
+    D.l.clear();
+    D.r.clear();
+    D.sum_nb.assign((size_t)b, 0);
+    D.size.assign((size_t)b, 1);
+    for (int64_t v = 0; v < b; v++) D.sum_nb[v] = nB[v];
+    std::vector<int32_t> uf((size_t)b), node_of((size_t)b);
+    for (int64_t v = 0; v < b; v++) uf[v] = node_of[v] = (int32_t)v;
+    auto find = [&](int32_t x) {
+        while (uf[x] != x) {
+            uf[x] = uf[uf[x]];
+            x = uf[x];
+        }
+        return x;
+    };
+    std::vector<int32_t> pre_a((size_t)ne), pre_b((size_t)ne);
+    for (int64_t lo = 0; lo < ne;) {
+        int64_t hi = lo;
+        while (hi + 1 < ne && ew[hi + 1] == ew[lo]) hi++;  // a run, as the top-down walk groups it
+        for (int64_t i = lo; i <= hi; i++) {
+            pre_a[i] = node_of[find(ea[i])];
+            pre_b[i] = node_of[find(eb[i])];
+        }
+        for (int64_t i = lo; i <= hi; i++) {
+            if (ea[i] == eb[i]) continue;
+            int32_t x = find(ea[i]), y = find(eb[i]);
+            if (x == y) return 1;  // a cycle: not a tree
+            const int32_t nx = node_of[x], ny = node_of[y];
+            const int32_t k = (int32_t)(b + (int64_t)D.l.size());
+            D.l.push_back(nx);
+            D.r.push_back(ny);
+            D.sum_nb.push_back(D.sum_nb[nx] + D.sum_nb[ny]);
+            D.size.push_back(D.size[nx] + D.size[ny]);
+            uf[y] = x;
+            node_of[x] = k;
+        }
+        lo = hi + 1;
+    }
+    // ---- top-down replay
+    std::vector<int32_t> group((size_t)b, 0), gsize(1, (int32_t)b), glabel(1, 1);
+    auto lab = [&](int32_t v) { return glabel[group[v]]; };
+    int32_t nextLabel = 2;
+    int64_t all = 0;
+    for (int64_t i = 0; i < b; i++) all += nB[i];
+    {
+        Cl root;
+        root.label = 1;
+        root.parent = -1;
+        root.birth = NAN;
+        root.numPoints = (int32_t)all;
+        clusters.push_back(root);
+    }
+    std::vector<int32_t> idx_of(2, -1);
+    idx_of[1] = 0;
+    std::vector<int32_t> pre((size_t)b, -1);  // pre-run node of an endpoint (this run)
+    std::vector<int32_t> stk;
+    struct Aff {
+        int32_t label;
+        int64_t order;
+        std::vector<int32_t> verts;
+    };
+    struct Piece {
+        int32_t g, node;
+    };
+    std::vector<Piece> pieces;
+    std::vector<int32_t> best_of_group;  // scratch: group -> index of its largest piece
+    int64_t cur = ne - 1;
+    while (cur >= 0) {
+        std::vector<Aff> aff;
+        const double cw = ew[cur];
+        const int64_t run_hi = cur;
+        while (cur >= 0 && ew[cur] == cw) {
+            const int32_t f = ea[cur], s = eb[cur];
+            pre[f] = pre_a[cur];
+            pre[s] = pre_b[cur];
+            if (lab(f) == 0) {
+                cur--;
+                continue;
+            }
+            size_t k = 0;
+            for (; k < aff.size(); k++)
+                if (aff[k].label == lab(f)) break;
+            if (k == aff.size()) aff.push_back(Aff{lab(f), (int64_t)aff.size(), {}});
+            for (int32_t v : {f, s}) {
+                auto &vs = aff[k].verts;
+                auto it = std::lower_bound(vs.begin(), vs.end(), v);
+                if (it == vs.end() || *it != v) vs.insert(it, v);
+            }
+            cur--;
+        }
+        // the run split live components into pieces: keep each component's largest piece in
+        // its group, move the others to fresh groups (labels unchanged)
+        pieces.clear();
+        for (int64_t i = cur + 1; i <= run_hi; i++) {
+            if (ea[i] == eb[i]) continue;
+            for (int32_t v : {ea[i], eb[i]}) {
+                const int32_t nd = (v == ea[i]) ? pre_a[i] : pre_b[i];
+                if (lab(v) == 0) continue;  // noise components are never relabelled
+                pieces.push_back(Piece{group[v], nd});
+            }
+        }
+        if (!pieces.empty()) {
+            std::sort(pieces.begin(), pieces.end(), [](const Piece &x, const Piece &y) {
+                return x.g < y.g || (x.g == y.g && x.node < y.node);
+            });
+            pieces.erase(std::unique(pieces.begin(), pieces.end(),
+                                     [](const Piece &x, const Piece &y) { return x.g == y.g && x.node == y.node; }),
+                         pieces.end());
+            for (size_t a = 0; a < pieces.size();) {
+                size_t e = a;
+                size_t big = a;
+                while (e < pieces.size() && pieces[e].g == pieces[a].g) {
+                    if (D.size[pieces[e].node] > D.size[pieces[big].node]) big = e;
+                    e++;
+                }
+                for (size_t q = a; q < e; q++) {
+                    if (q == big) continue;
+                    const int32_t ng = (int32_t)glabel.size();
+                    glabel.push_back(glabel[pieces[q].g]);
+                    gsize.push_back(D.size[pieces[q].node]);
+                    gsize[pieces[q].g] -= D.size[pieces[q].node];
+                    D.leaves(pieces[q].node, stk, [&](int32_t v) { group[v] = ng; });
+                }
+                a = e;
+            }
+        }
+        if (aff.empty()) continue;
+        int64_t cap = 16;
+        while ((int64_t)aff.size() > cap * 3 / 4) cap *= 2;
+        std::stable_sort(aff.begin(), aff.end(), [&](const Aff &x, const Aff &y) {
+            uint32_t bx = jhash(x.label) & (uint32_t)(cap - 1), by = jhash(y.label) & (uint32_t)(cap - 1);
+            if (bx != by) return bx < by;
+            return x.order < y.order;
+        });
+        for (auto &A : aff) {
+            const int32_t parentLabel = A.label;
+            std::vector<Cl> newc;
+            for (int32_t rootV : A.verts) {
+                const int32_t nd = pre[rootV];
+                const int64_t countMembers = D.sum_nb[nd];
+                if (countMembers >= mcl) {
+                    Cl c;
+                    c.label = parentLabel;
+                    c.parent = parentLabel;
+                    c.birth = cw;
+                    c.numPoints = (int32_t)countMembers;
+                    c.node = nd;
+                    c.members.push_back(rootV);  // any member: locates the piece's group
+                    newc.push_back(std::move(c));
+                } else {
+                    glabel[group[rootV]] = 0;  // the piece is exactly this group
+                    const int32_t ci = parentLabel < (int32_t)idx_of.size() ? idx_of[parentLabel] : -1;
+                    if (ci >= 0 && clusters[ci].death == JMAX) {
+                        int rc = detach(clusters[ci], (int32_t)countMembers, cw);
+                        if (rc) return rc;
+                    }
+                }
+            }
+            if (newc.size() >= 2) {
+                for (auto &c : newc) {
+                    c.label = nextLabel;
+                    glabel[group[c.members[0]]] = nextLabel;
+                    c.members.clear();
+                    nextLabel++;
+                    const int32_t pi = c.parent < (int32_t)idx_of.size() ? idx_of[c.parent] : -1;
+                    if (pi >= 0 && clusters[pi].death == JMAX) {
+                        clusters[pi].hasChildren = true;
+                        int rc = detach(clusters[pi], c.numPoints, c.birth);
+                        if (rc) return rc;
+                    }
+                    if ((int32_t)idx_of.size() <= c.label) idx_of.resize((size_t)c.label + 1, -1);
+                    idx_of[c.label] = (int32_t)clusters.size();
+                    clusters.push_back(std::move(c));
+                }
+            }
+        }
+    }
+    return HDB_OK;
+}
+
+static int construct_cluster_tree_bfs(int64_t b, const int32_t *ea, const int32_t *eb, const double *ew, int64_t ne,
                                   int32_t mcl, const int32_t *nB, std::vector<Cl> &clusters) {
     std::vector<std::vector<int32_t>> adj(b);
     for (int64_t i = 0; i < ne; i++) {
@@ -311,7 +533,7 @@ static int construct_cluster_tree(int64_t b, const int32_t *ea, const int32_t *e
 }
 
 static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *eB, const double *nnB, int64_t b,
-                          int d, int metric, int32_t *flat) {
+                          int d, int metric, int32_t *flat, const Dendro *D) {
     // clusterTree.remove(0)
     std::vector<Cl *> tree;
     for (size_t i = 1; i < cl.size(); i++) tree.push_back(&cl[i]);
@@ -409,12 +631,18 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
             sol[key] = 0;
         }
     }
+    std::vector<int32_t> stk;
     for (auto *c : sorted)
-        if (sol[c->label])
+        if (sol[c->label]) {
+            if (c->node >= 0 && D) {
+                D->leaves(c->node, stk, [&](int32_t m) { flat[m] = c->label; });
+                continue;
+            }
             for (int32_t m : c->members) {
                 if (m < 0 || m >= b) return HDB_EREF_OOB;
                 flat[m] = c->label;
             }
+        }
     // noise -> first later-valid neighbour in index order (:485-502)
     for (int64_t p = 0; p < b; p++) {
         double minD = JMAX;
@@ -450,12 +678,18 @@ int local_model_host(const double *rep, const double *eB, const double *nnB, con
     if (rc) return rc;
     auto t1 = clk::now();
     std::vector<Cl> cl;
-    rc = construct_cluster_tree(b, mva, mvb, mw, ne, min_cl_size, nB, cl);
+    Dendro D;
+    rc = construct_cluster_tree_fast(b, mva, mvb, mw, ne, min_cl_size, nB, cl, D);
+    const bool fast = rc != 1;
+    if (!fast) {  // not a forest: the reference's BFS walk
+        cl.clear();
+        rc = construct_cluster_tree_bfs(b, mva, mvb, mw, ne, min_cl_size, nB, cl);
+    }
     auto t2 = clk::now();
     g_lm_us[0] += us(t0, t1);
     g_lm_us[1] += us(t1, t2);
     if (rc) return rc;
-    rc = find_prominent(cl, rep, eB, nnB, b, d, metric, labels);
+    rc = find_prominent(cl, rep, eB, nnB, b, d, metric, labels, fast ? &D : nullptr);
     g_lm_us[2] += us(t2, clk::now());
     if (rc) return rc;
     int64_t k = 0;

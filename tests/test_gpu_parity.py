@@ -397,3 +397,38 @@ def test_knn_fp32_screen_equals_fp64_path(pkg, oracle, scale):
         b = star.calculateCoreDistances(X, 4, None, sem)
         ctx.set_option("knn_fp32_screen", 1)
         assert eq(a, ref) and eq(b, ref), sem
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_local_model_stress_vs_oracle(pkg, oracle, case):
+    """Random bubble sets over tie-heavy inputs (integer grids, Skin duplicates, blobs):
+    the dendrogram-replay cluster tree must reproduce the reference's BFS walk exactly --
+    labels, sorted MST, inter-cluster edges, or the same exception."""
+    rng = np.random.default_rng(1000 + case)
+    kind = case % 3
+    n = int(rng.integers(300, 6000))
+    if kind == 0:
+        X = rng.integers(0, 6, size=(n, 2)).astype(np.float64)  # heavy exact ties
+    elif kind == 1:
+        X = load_skin(n)
+    else:
+        X = blobs(n, 3, int(rng.integers(2, 9)), case)
+    m = int(rng.integers(20, max(21, n // 3)))
+    sids = np.sort(rng.choice(n, m, replace=False))
+    near, _ = oracle.nearest_sample(X, X[sids])
+    used = np.unique(near)
+    remap = -np.ones(m, np.int32)
+    remap[used] = np.arange(used.shape[0], dtype=np.int32)
+    st = oracle.bubble_stats(X, remap[near], used.shape[0])
+    min_pts = int(rng.choice([2, 4, 8]))
+    mcl = int(rng.choice([2, 4, 16, 64]))
+    try:
+        lm = oracle.local_model(st["rep"], st["info"], min_pts, mcl)
+    except oracle.OracleError as e:
+        with pytest.raises(pkg.HdbError) as ei:
+            pkg.LocalModelReduceByKey(min_pts, mcl).call(st["rep"], st["info"])
+        assert ei.value.code == e.code
+        return
+    labels, mst, inter = pkg.LocalModelReduceByKey(min_pts, mcl).call(st["rep"], st["info"])
+    assert eq(labels, lm["labels"]) and eq(mst.getEges(), lm["mst"][2]) and eq(inter[2], lm["inter"][2])
+    assert eq(inter[0], lm["inter"][0]) and eq(inter[1], lm["inter"][1])
