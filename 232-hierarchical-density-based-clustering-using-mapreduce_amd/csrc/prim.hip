@@ -337,6 +337,141 @@ __global__ void prim_step_final_kernel(PrimIn in, const int64_t *__restrict__ of
 }
 
 // ------------------------------------------------------------------ host
+
+// --------------------------------------------------- cooperative kernel
+// One partition of 4096 < n <= 65536 vertices (bubble models of the C3/C5 configs): one
+// lane per vertex over ceil(n / BS) co-resident workgroups (cooperative launch), the whole
+// Prim in one launch.  Each step: update + workgroup argmin, publish the partial, one
+// grid barrier (monotone counter), every workgroup folds the nwg partials (argmin_last is
+// associative and commutative, so all agree on the next vertex).  Partials are double
+// buffered by step parity: a workgroup can be at most one step ahead of any other.
+// Partial reads use agent-scope atomic loads (bypass the non-coherent L1).
+template <int BS>
+__global__ __launch_bounds__(BS) void prim_coop_kernel(PrimIn in, int n, int self_edges, int32_t *__restrict__ va,
+                                                       int32_t *__restrict__ vb, double *__restrict__ w,
+                                                       unsigned long long *__restrict__ part, unsigned *counter,
+                                                       int *err) {
+    constexpr int NW = BS / 64;
+    __shared__ double s_v[NW];
+    __shared__ int s_i[NW];
+    __shared__ int s_cur;
+    const int nwg = (int)gridDim.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int i = (int)blockIdx.x * BS + tid;
+    double best = JMAX;
+    int par = 0;
+    bool att = (i >= n) || (i == n - 1);
+    int cur = n - 1;
+    for (int step = 1; step < n; step++) {
+        double lv = INFINITY;
+        int li = -1;
+        if (!att) {
+            double mrd;
+            if (mrd_improves(in, cur, i, best, mrd)) {
+                best = mrd;
+                par = in.ids[cur];
+            }
+            argmin_last(lv, li, best, i);
+        }
+        wave_argmin_last(lv, li);
+        if (lane == 0) {
+            s_v[wid] = lv;
+            s_i[wid] = li;
+        }
+        __syncthreads();
+        const int buf = step & 1;
+        if (tid == 0) {
+            double v = s_v[0];
+            int ii = s_i[0];
+#pragma unroll
+            for (int q = 1; q < NW; q++) argmin_last(v, ii, s_v[q], s_i[q]);
+            __hip_atomic_store(&part[2 * (buf * nwg + blockIdx.x)], (unsigned long long)__double_as_longlong(v),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&part[2 * (buf * nwg + blockIdx.x) + 1], (unsigned long long)(unsigned)ii,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned target = (unsigned)step * (unsigned)nwg;
+            unsigned spins = 0;
+            while (__hip_atomic_load(counter, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                if (++spins > (1u << 26)) {  // a co-residency failure must not hang the device
+                    atomicExch(err, 1);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        if (wid == 0) {
+            double v = INFINITY;
+            int ii = -1;
+            for (int k = lane; k < nwg; k += 64) {
+                const unsigned long long bv =
+                    __hip_atomic_load(&part[2 * (buf * nwg + k)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long bi =
+                    __hip_atomic_load(&part[2 * (buf * nwg + k) + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                argmin_last(v, ii, __longlong_as_double((long long)bv), (int)(unsigned)bi);
+            }
+            wave_argmin_last(v, ii);
+            if (lane == 0) s_cur = ii;
+        }
+        __syncthreads();
+        cur = s_cur;
+        if (cur < 0) break;  // unreachable (an unattached vertex always exists) -- uniform exit
+        if (i == cur) att = true;
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    }
+    if (i < n - 1) {
+        va[i] = par;
+        vb[i] = in.ids[i];
+        w[i] = best;
+    }
+    if (self_edges && i < n) {
+        va[n - 1 + i] = in.ids[i];
+        vb[n - 1 + i] = in.ids[i];
+        w[n - 1 + i] = in.core[i];
+    }
+}
+
+static bool launch_coop(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
+                        int32_t *va, int32_t *vb, double *w) {
+    constexpr int BS = 1024;
+    const int nwg = (int)ceil_div(n, BS);
+    if (n > 65536 || nwg < 1) return false;
+    int coop = 0, ncu = 0, per_cu = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device));
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, prim_coop_kernel<BS>, BS, 0));
+    if (!coop || (int64_t)per_cu * ncu < nwg) return false;
+    // scratch: partials [2][nwg] x (value, index), barrier counter, error flag
+    char *base = (char *)arena(ctx, A_WORK3, 16 * 2 * (size_t)nwg + 512);
+    unsigned long long *part = (unsigned long long *)base;
+    unsigned *counter = (unsigned *)(base + 16 * 2 * (size_t)nwg + 256);
+    int *err = (int *)(counter + 16);
+    HIP_CHECK(hipMemsetAsync(counter, 0, 256, ctx->stream));
+    PrimIn L = in;
+    L.X = in.X + o * in.d;
+    L.core = in.core + o;
+    L.ids = in.ids + o;
+    if (in.eB) {
+        L.eB = in.eB + o;
+        L.nnB = in.nnB + o;
+    }
+    int nn = (int)n;
+    int32_t *pva = va + eo, *pvb = vb + eo;
+    double *pw = w + eo;
+    void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &part, &counter, &err};
+    {
+        KernelTimer t(ctx, "prim_coop");
+        HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_coop_kernel<BS>, dim3(nwg), dim3(BS), args, 0,
+                                             ctx->stream));
+    }
+    int h_err = 0;
+    HIP_CHECK(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (h_err) HDB_THROW(HDB_EDEVICE, "prim_coop: grid barrier timed out (workgroups not co-resident)");
+    return true;
+}
+
 template <int BS, int PPT>
 static void launch_block(hdb_ctx *ctx, const PrimIn &in, const int64_t *offs, const int64_t *eoff,
                          const int32_t *parts, int np, int self_edges, int32_t *va, int32_t *vb, double *w) {
@@ -377,6 +512,15 @@ void prim_batched_device(hdb_ctx *ctx, const PrimIn &in, const int64_t *h_offs, 
     };
     size_t o_off = carve(sizeof(int64_t) * (P + 1)), o_eoff = carve(sizeof(int64_t) * (P + 1));
     size_t o_parts = carve(sizeof(int32_t) * (P + 1));
+    // cooperative single-launch Prim for 4096 < n <= 65536 when the device allows it
+    if (ctx->prim_coop) {
+        std::vector<int32_t> rest;
+        for (int32_t p : cls[4]) {
+            int64_t n = h_offs[p + 1] - h_offs[p];
+            if (!launch_coop(ctx, in, h_offs[p] - h_offs[0], n, eoff[p], self_edges, va, vb, w)) rest.push_back(p);
+        }
+        cls[4].swap(rest);
+    }
     // stepwise state
     std::vector<int32_t> wg_part, wg_first(P, 0), wg_count(P, 0);
     constexpr int SBS = 256, SPPT = 4;

@@ -432,3 +432,22 @@ def test_local_model_stress_vs_oracle(pkg, oracle, case):
     labels, mst, inter = pkg.LocalModelReduceByKey(min_pts, mcl).call(st["rep"], st["info"])
     assert eq(labels, lm["labels"]) and eq(mst.getEges(), lm["mst"][2]) and eq(inter[2], lm["inter"][2])
     assert eq(inter[0], lm["inter"][0]) and eq(inter[1], lm["inter"][1])
+
+
+@pytest.mark.parametrize("n,kind", [(4097, "blobs"), (12000, "blobs"), (30000, "blobs"), (20000, "skin")])
+def test_prim_cooperative_vs_oracle(pkg, oracle, n, kind):
+    """4096 < n <= 65536: the single-launch cooperative Prim (grid barrier per step) must be
+    the reference Prim exactly, ties included (Skin: pervasive zero-weight ties); the
+    stepwise multi-launch path must agree with it."""
+    X = load_skin(n) if kind == "skin" else blobs(n, 3, 7, n)
+    core = oracle.core_distances(X, 4, semantics=0)
+    va, vb, w = oracle.prim_mst(X, core)
+    ctx = pkg.Context.get(0)
+    star = pkg.HDBSCANStar(ctx)
+    for coop in (1, 0):
+        ctx.set_option("prim_coop", coop)
+        try:
+            g = star.constructMST(X, core, True)
+        finally:
+            ctx.set_option("prim_coop", 1)
+        assert eq(g.getVerticeA(), va) and eq(g.getVericeB(), vb) and eq(g.getEges(), w), coop
