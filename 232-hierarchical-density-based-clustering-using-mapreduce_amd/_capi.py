@@ -91,6 +91,7 @@ def lib():
             "hdb_prim_mst_batched": [vp, dp, lp, i32, i32, dp, ip, i32, i32, ip, ip, dp],
             "hdb_leaf_msts": [vp, dp, lp, i32, i32, ip, i32, i32, dp, ip, ip, dp],
             "hdb_mst_boruvka": [vp, dp, i64, i32, dp, i32, i32, ip, ip, dp],
+            "hdb_exact_mst": [vp, dp, i64, i32, i32, i32, i32, i32, dp, ip, ip, dp],
             "hdb_nearest_sample": [vp, dp, i64, dp, i64, i32, i32, ip, ip, ip, dp],
             "hdb_bubble_stats": [vp, dp, i64, i32, ip, i64, i32, dp, dp, dp, dp],
             "hdb_bubble_core_distances": [vp, dp, ip, dp, dp, i64, i32, i32, i32, dp],
@@ -115,7 +116,7 @@ def lib():
 EXPORTED = ["hdb_ctx_create", "hdb_ctx_destroy", "hdb_ctx_set_stream", "hdb_ctx_set_timing", "hdb_ctx_set_option",
             "hdb_ctx_get_stat", "hdb_ctx_kernel_time", "hdb_ctx_synchronize", "hdb_last_error", "hdb_version",
             "hdb_distance_rows", "hdb_core_distances", "hdb_knn", "hdb_prim_mst", "hdb_prim_mst_batched",
-            "hdb_leaf_msts", "hdb_mst_boruvka", "hdb_nearest_sample", "hdb_bubble_stats",
+            "hdb_leaf_msts", "hdb_mst_boruvka", "hdb_exact_mst", "hdb_nearest_sample", "hdb_bubble_stats",
             "hdb_bubble_core_distances", "hdb_bubble_prim_mst", "hdb_local_model", "hdb_quicksort_edges",
             "hdb_sort_edges_desc", "hdb_flat_labels"]
 

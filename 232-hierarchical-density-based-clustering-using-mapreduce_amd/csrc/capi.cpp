@@ -240,6 +240,23 @@ int hdb_mst_boruvka(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const d
     });
 }
 
+int hdb_exact_mst(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t min_pts, int32_t metric,
+                  int32_t semantics, int32_t self_edges, double *core_out, int32_t *va, int32_t *vb, double *w) {
+    return guarded(ctx, [&] {
+        check_metric(metric);
+        if (n < 1 || d <= 0 || !X || !va || !vb || !w) HDB_THROW(HDB_EINVAL, "bad arguments");
+        if (semantics < 0 || semantics > 2) HDB_THROW(HDB_EINVAL, "unknown core semantics");
+        const int64_t ne = (n - 1) + (self_edges ? n : 0);
+        Stager s(ctx);
+        const double *dX = s.in(X, n * d);
+        double *dc = core_out ? s.out(core_out, n) : (double *)arena(ctx, A_STAGE_OUT, sizeof(double) * (size_t)n);
+        int32_t *dva = s.out(va, ne), *dvb = s.out(vb, ne);
+        double *dw = s.out(w, ne);
+        exact_leaf_device(ctx, dX, n, d, min_pts, metric, semantics, dc, self_edges, dva, dvb, dw);
+        s.finish();
+    });
+}
+
 int hdb_nearest_sample(hdb_ctx *ctx, const double *X, int64_t n, const double *S, int64_t m, int32_t d,
                        int32_t metric, const int32_t *x_key, const int32_t *s_key, int32_t *nearest_out,
                        double *dist_out) {

@@ -17,6 +17,16 @@ struct PrimIn {
 void pack_rows(hdb_ctx *ctx, const double *X, int64_t n, int d, int dp, double *Xp);
 void knn_lists_device(hdb_ctx *ctx, const double *X_dev, int64_t n, int d, int k, int metric, bool excl,
                       double *lists_v, int32_t *lists_i, int *KC_out);
+void core_epilogue_device(hdb_ctx *ctx, const double *lists, int64_t n, int KC, int K, int semantics, double *core);
+// list bucket for k neighbours (K1/K1t keep KC >= k values per row)
+inline int pick_kc(int k) {
+    if (k <= 1) return 1;
+    if (k <= 3) return 3;
+    if (k <= 7) return 7;
+    if (k <= 15) return 15;
+    if (k <= 31) return 31;
+    return -1;
+}
 void core_distances_device(hdb_ctx *ctx, const double *X_dev, int64_t n, int d, int min_pts, int metric,
                            int semantics, double *core);
 void prim_batched_device(hdb_ctx *ctx, const PrimIn &in, const int64_t *h_offs, int P, int self_edges, int32_t *va,
@@ -34,6 +44,8 @@ void distance_rows_device(hdb_ctx *ctx, const double *a, const double *b, int64_
 bool knn_tree_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC, bool excl, double *lists);
 // self edges (v, v, core[v]) as FirstStep emits them after the tree edges (HDBSCANStar.java:190-203)
 void self_edges_device(hdb_ctx *ctx, const double *core, int64_t n, int32_t *va, int32_t *vb, double *w);
+void exact_leaf_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int min_pts, int metric, int semantics,
+                       double *core, int self_edges, int32_t *va, int32_t *vb, double *w);
 void boruvka_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const double *core, int metric, int32_t *va,
                     int32_t *vb, double *w);
 

@@ -266,21 +266,9 @@ void knn_lists_device(hdb_ctx *ctx, const double *X_dev, int64_t n, int d, int k
     HIP_CHECK(hipGetLastError());
 }
 
-// core distances on device buffers
-void core_distances_device(hdb_ctx *ctx, const double *X_dev, int64_t n, int d, int min_pts, int metric,
-                           int semantics, double *core) {
-    if (min_pts < 1) HDB_THROW(HDB_EINVAL, "minPts must be >= 1");
-    if (n == 0) return;
-    if (min_pts == 1) {  // HDBSCANStar.java:75-77
-        HIP_CHECK(hipMemsetAsync(core, 0, sizeof(double) * (size_t)n, ctx->stream));
-        return;
-    }
-    int K = min_pts - 1;
-    int KC = pick_kc(K);
-    if (KC < 0) HDB_THROW(HDB_EINVAL, "minPts too large (max 32)");
-    double *lists = (double *)arena(ctx, A_WORK0, sizeof(double) * (size_t)(n * KC));
-    bool excl = semantics == HDB_CORE_EXCL_SELF;
-    knn_lists_device(ctx, X_dev, n, d, K, metric, excl, lists, nullptr, &KC);
+// core distances from per-row lists (n x KC, ascending, MAX padded): element K-1 per row,
+// or the cumulative prefix merge of INCL_SELF_CUMULATIVE (HDBSCANStar.java:79-103)
+void core_epilogue_device(hdb_ctx *ctx, const double *lists, int64_t n, int KC, int K, int semantics, double *core) {
     int g = (int)std::min<int64_t>(ceil_div(n, 256), 4096);
     if (semantics != HDB_CORE_INCL_SELF_CUMULATIVE) {
         hipLaunchKernelGGL(core_from_lists_kernel, dim3(g), dim3(256), 0, ctx->stream, lists, n, KC, K, core);
@@ -289,7 +277,7 @@ void core_distances_device(hdb_ctx *ctx, const double *X_dev, int64_t n, int d, 
     }
     const int64_t CH = 256;
     int64_t nch = ceil_div(n, CH);
-    double *agg = (double *)arena(ctx, A_WORK1, sizeof(double) * (size_t)(nch * 32));
+    double *agg = (double *)arena(ctx, A_WORK2, sizeof(double) * (size_t)(nch * 32));
     int gc = (int)std::min<int64_t>(ceil_div(nch, 64), 4096);
 #define CUM_CASE(KK)                                                                                          \
     case KK:                                                                                                  \
@@ -308,6 +296,24 @@ void core_distances_device(hdb_ctx *ctx, const double *X_dev, int64_t n, int d, 
     }
 #undef CUM_CASE
     HIP_CHECK(hipGetLastError());
+}
+
+// core distances on device buffers
+void core_distances_device(hdb_ctx *ctx, const double *X_dev, int64_t n, int d, int min_pts, int metric,
+                           int semantics, double *core) {
+    if (min_pts < 1) HDB_THROW(HDB_EINVAL, "minPts must be >= 1");
+    if (n == 0) return;
+    if (min_pts == 1) {  // HDBSCANStar.java:75-77
+        HIP_CHECK(hipMemsetAsync(core, 0, sizeof(double) * (size_t)n, ctx->stream));
+        return;
+    }
+    int K = min_pts - 1;
+    int KC = pick_kc(K);
+    if (KC < 0) HDB_THROW(HDB_EINVAL, "minPts too large (max 32)");
+    double *lists = (double *)arena(ctx, A_WORK0, sizeof(double) * (size_t)(n * KC));
+    bool excl = semantics == HDB_CORE_EXCL_SELF;
+    knn_lists_device(ctx, X_dev, n, d, K, metric, excl, lists, nullptr, &KC);
+    core_epilogue_device(ctx, lists, n, KC, K, semantics, core);
 }
 
 }  // namespace hdb

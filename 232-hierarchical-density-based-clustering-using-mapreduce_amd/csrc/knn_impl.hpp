@@ -327,14 +327,6 @@ __global__ void knn_merge_kernel(const double *__restrict__ part_v, const int32_
 }
 
 // ----------------------------------------------------------------- host
-inline int pick_kc(int k) {
-    if (k <= 1) return 1;
-    if (k <= 3) return 3;
-    if (k <= 7) return 7;
-    if (k <= 15) return 15;
-    if (k <= 31) return 31;
-    return -1;
-}
 
 struct KnnPlan {
     int Q;

@@ -355,6 +355,7 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
                                                           Bvh bvh, unsigned long long *__restrict__ comp_w,
                                                           double *__restrict__ best_w, double *__restrict__ best_s,
                                                           int32_t *__restrict__ best_lo, int32_t *__restrict__ best_hi,
+                                                          const uint8_t *__restrict__ done,
                                                           unsigned long long *__restrict__ stats) {
     __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
     const int w = threadIdx.x >> 6;
@@ -400,8 +401,9 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
         }
     };
     auto bound = [&]() -> double { return sb < cb2 ? sb : cb2; };
+    const bool search = valid && !(done && done[i]);  // a done lane's seed is its exact best
     auto needs_box = [&](const double *lo, const double *hi, int32_t tg) -> bool {
-        if (!valid) return false;
+        if (!search) return false;
         if (tg >= 0 && tg == mcomp) return false;
         const double bd = bound();
         if (!(bd < INFINITY)) return true;
@@ -589,15 +591,18 @@ __global__ void seed_kernel(const Rec<D> *__restrict__ recs, int64_t n, const in
 
 __global__ void fill_inf_kernel(double *__restrict__ p, int64_t n) { HDB_GRID_STRIDE(i, n) p[i] = INFINITY; }
 
-__global__ void jump_kernel(int32_t *__restrict__ parent, int64_t n, int *__restrict__ changed) {
+// parent pointers -> the root of each hook tree in one launch (chains only shorten while
+// other lanes write: every value read is an ancestor, so the walk always ends at the root)
+__global__ void resolve_kernel(int32_t *__restrict__ parent, int64_t n) {
     HDB_GRID_STRIDE(c, n) {
         int32_t p = parent[c];
         if (p < 0) continue;
-        int32_t pp = parent[p];
-        if (pp != p) {
-            parent[c] = pp;
-            *changed = 1;
+        while (true) {
+            const int32_t pp = __hip_atomic_load(&parent[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (pp == p) break;
+            p = pp;
         }
+        parent[c] = p;
     }
 }
 
@@ -634,15 +639,70 @@ __global__ void edge_out_kernel(const int32_t *perm_, const int32_t *a, const in
     }
 }
 
+// ------------------------------------------------ fused leaf: kNN-seeded round 0
+template <int D>
+__global__ void set_core_kernel(Rec<D> *__restrict__ recs, int64_t n, const double *__restrict__ core) {
+    HDB_GRID_STRIDE(i, n) recs[i].core = core[recs[i].id];
+}
+
+// Round-0 Boruvka seed from the K nearest neighbours K1t just found (sorted positions,
+// squared distances): the best (w, s, lo, hi) among them is a valid candidate, and it is
+// provably the lane's exact best when no other point can beat it: every point outside the
+// list has s' >= s_K (the list holds all points with s' < s_K), so its weight is
+// >= LB = max(fl(sqrt(s_K)), core_p); the seed is exact if w < LB, or w == LB and s < s_K.
+// Exact lanes skip the round-0 traversal.
+template <int D, int K>
+__global__ void knn_seed_kernel(const Rec<D> *__restrict__ recs, int64_t n, const int32_t *__restrict__ nb_pos,
+                                const double *__restrict__ nb_s, double *__restrict__ best_w, double *__restrict__ best_s,
+                                int32_t *__restrict__ best_lo, int32_t *__restrict__ best_hi,
+                                uint8_t *__restrict__ done) {
+    HDB_GRID_STRIDE(i, n) {
+        const double mcore = recs[i].core;
+        const int32_t mid = recs[i].id;
+        Best b{INFINITY, INFINITY, INT32_MAX, INT32_MAX};
+        double sK = -INFINITY;
+        bool full = true;
+        for (int k = 0; k < K; k++) {
+            const int32_t j = nb_pos[i * K + k];
+            const double s = nb_s[i * K + k];
+            if (j < 0 || !(s < INFINITY)) {
+                full = false;
+                continue;
+            }
+            sK = s > sK ? s : sK;
+            if (j == (int32_t)i) continue;  // INCL lists hold the point itself
+            double mrd = sqrt(s);  // HDBSCANStar.java:162-168 order, as the scan kernel
+            if (mcore > mrd) mrd = mcore;
+            const double oc = recs[j].core;
+            if (oc > mrd) mrd = oc;
+            const int32_t oid = recs[j].id;
+            const int32_t lo = mid < oid ? mid : oid, hi = mid < oid ? oid : mid;
+            if (key_less(mrd, s, lo, hi, b)) b = Best{mrd, s, lo, hi};
+        }
+        bool exact = false;
+        if (full && b.w < INFINITY) {
+            double lb = sqrt(sK);
+            if (mcore > lb) lb = mcore;
+            exact = (b.w < lb) || (b.w == lb && b.s < sK);
+        }
+        best_w[i] = b.w;
+        best_s[i] = b.s;
+        best_lo[i] = b.lo;
+        best_hi[i] = b.hi;
+        done[i] = exact ? 1 : 0;
+    }
+}
+
 // ------------------------------------------------------------ K1t: tree kNN
 // A wave owns query tile t (lane = point).  Its own tile is scanned first (it holds the
 // nearest candidates in Morton order, so the K-th bound is tight from the start), then the
 // BVH is walked nearest-first, skipping any node whose box no lane can still improve on.
 // Candidates are wave-uniform (scalar loads); each lane evaluates the exact FP64 squared
 // distance in the reference's order and feeds the register top-K network.
-template <int D, int K>
+template <int D, int K, bool IDX>
 __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
                                                        Bvh bvh, int excl, double *__restrict__ lists,
+                                                       int32_t *__restrict__ nb_pos, double *__restrict__ nb_s,
                                                        unsigned long long *__restrict__ stats) {
     __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
     const int w = threadIdx.x >> 6;
@@ -664,8 +724,12 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
         for (int c = 0; c < D; c++) mx[c] = 0;
     }
     double buf[K];
+    int bix[K];
 #pragma unroll
-    for (int k = 0; k < K; k++) buf[k] = INFINITY;
+    for (int k = 0; k < K; k++) {
+        buf[k] = INFINITY;
+        bix[k] = -1;
+    }
     const int32_t skip_self = excl ? mid : -2;
     unsigned long long nev = 0, n_leaf = 0, n_node = 0;
 
@@ -688,7 +752,8 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
 #pragma unroll
                 for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
                 if (r.id == skip_self) s = INFINITY;
-                topk_insert<K>(buf, s);
+                if (IDX) topk_insert_idx<K>(buf, bix, s, (int)q);
+                else topk_insert<K>(buf, s);
             }
         }
     };
@@ -715,6 +780,10 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
         for (int k = 0; k < K; k++) {
             const double v = buf[k];
             lists[(int64_t)mid * K + k] = (v < INFINITY) ? sqrt(v) : JMAX;  // Java keeps Double.MAX_VALUE
+            if (IDX) {  // sorted-position neighbour list (squared distances) for the MST seeds
+                nb_pos[i * K + k] = bix[k];
+                nb_s[i * K + k] = v;
+            }
         }
     }
     if (stats) {
@@ -845,8 +914,8 @@ static void knn_tree_impl(hdb_ctx *ctx, const double *X, int64_t n, bool excl, d
     if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 24, ctx->stream));
     {
         KernelTimer t(ctx, "knn_tree");
-        hipLaunchKernelGGL((knn_tree_kernel<D, K>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256), 0, ctx->stream,
-                           sp.recs, n, sp.ntiles, sp.bvh, excl ? 1 : 0, lists, evals);
+        hipLaunchKernelGGL((knn_tree_kernel<D, K, false>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256), 0,
+                           ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, excl ? 1 : 0, lists, nullptr, nullptr, evals);
         HIP_CHECK(hipGetLastError());
     }
     if (evals) {
@@ -885,27 +954,68 @@ bool knn_tree_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC, bo
 }
 
 // ------------------------------------------------------------------- K2b host
+// per-round Boruvka state carved after the index: comp_w, comp_key, comp_s, best_w, best_s
+// (8n each), best_lo/hi, parent, parent2, is_root (4n each), counters, edge lists
+static size_t boruvka_extra_bytes(int64_t n) {
+    const size_t per = (size_t)n;
+    auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
+    return 5 * rnd(8 * per) + 5 * rnd(4 * per) + 3 * 256 + 2 * rnd(4 * per) + rnd(8 * per) + 256;
+}
+
+// Boruvka rounds over a built index whose records carry the core distances.  extra: the
+// boruvka_extra_bytes(n) region.  seeded: best_* (first 8n/4n arrays of extra) already hold
+// round-0 seeds (done0: lanes whose seed is exact skip the round-0 traversal).
+template <int D>
+static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extra, bool seeded,
+                             const uint8_t *done0, int32_t *va, int32_t *vb, double *w);
+
+template <int D>
+struct BoruvkaState {
+    unsigned long long *comp_w, *comp_key, *comp_s;
+    double *best_w, *best_s;
+    int32_t *best_lo, *best_hi;
+};
+template <int D>
+static BoruvkaState<D> boruvka_state(char *extra, int64_t n, size_t *used = nullptr) {
+    Carve ex;
+    ex.base = extra;
+    const size_t per = (size_t)n;
+    BoruvkaState<D> b;
+    b.best_w = ex.take<double>(per);
+    b.best_s = ex.take<double>(per);
+    b.best_lo = ex.take<int32_t>(per);
+    b.best_hi = ex.take<int32_t>(per);
+    b.comp_w = ex.take<unsigned long long>(per);
+    b.comp_key = ex.take<unsigned long long>(per);
+    b.comp_s = ex.take<unsigned long long>(per);
+    if (used) *used = ex.off;
+    return b;
+}
+
 template <int D>
 static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double *core, int32_t *va, int32_t *vb,
                          double *w) {
     Carve cv;
     char *extra = nullptr;
-    // per-round state after the index: comp_w, comp_key (8n each), best_w (8n), best_lo/hi,
-    // parent, parent2, is_root (4n each), counters, edge lists (4n, 4n, 8n)
-    const size_t per = (size_t)n;
-    auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t extra_bytes = 5 * rnd(8 * per) + 5 * rnd(4 * per) + 3 * 256 + 2 * rnd(4 * per) + rnd(8 * per);
     KernelTimer tt(ctx, "boruvka_total");
-    Spatial<D> sp = build_spatial_in<D>(ctx, A_WORK0, X, n, core, cv, extra_bytes, &extra);
-    Carve ex;
+    Spatial<D> sp = build_spatial_in<D>(ctx, A_WORK0, X, n, core, cv, boruvka_extra_bytes(n), &extra);
+    boruvka_on_index<D>(ctx, sp, n, extra, false, nullptr, va, vb, w);
+}
+
+template <int D>
+static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extra, bool seeded,
+                             const uint8_t *done0, int32_t *va, int32_t *vb, double *w) {
+    const size_t per = (size_t)n;
+    size_t used = 0;
+    BoruvkaState<D> bs = boruvka_state<D>(extra, n, &used);
+    Carve ex;  // the rest of the region, after the BoruvkaState arrays
     ex.base = extra;
-    unsigned long long *comp_w = ex.take<unsigned long long>(per), *comp_key = ex.take<unsigned long long>(per);
-    double *best_w = ex.take<double>(per), *best_s = ex.take<double>(per);
-    unsigned long long *comp_s = ex.take<unsigned long long>(per);
-    int32_t *best_lo = ex.take<int32_t>(per), *best_hi = ex.take<int32_t>(per);
+    ex.off = used;
+    unsigned long long *comp_w = bs.comp_w, *comp_key = bs.comp_key, *comp_s = bs.comp_s;
+    double *best_w = bs.best_w, *best_s = bs.best_s;
+    int32_t *best_lo = bs.best_lo, *best_hi = bs.best_hi;
     int32_t *parent = ex.take<int32_t>(per), *parent2 = ex.take<int32_t>(per), *is_root = ex.take<int32_t>(per);
     unsigned long long *n_edges = ex.take<unsigned long long>(1);
-    int *changed = ex.take<int>(1);
     int32_t *ea = ex.take<int32_t>(per), *eb = ex.take<int32_t>(per);
     double *ew = ex.take<double>(per);
     unsigned long long *evals = ctx->count_evals ? ex.take<unsigned long long>(3) : nullptr;
@@ -918,7 +1028,7 @@ static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double 
     const int g = (int)std::min<int64_t>(ceil_div(n, 256), 4096);
     hipStream_t st = ctx->stream;
     HIP_CHECK(hipMemsetAsync(n_edges, 0, 8, st));
-    hipLaunchKernelGGL(fill_inf_kernel, dim3(g), dim3(256), 0, st, best_w, n);
+    if (!seeded) hipLaunchKernelGGL(fill_inf_kernel, dim3(g), dim3(256), 0, st, best_w, n);
     HIP_CHECK(hipGetLastError());
 
     static const char *round_names[] = {"boruvka_r0", "boruvka_r1", "boruvka_r2", "boruvka_r3", "boruvka_r4",
@@ -943,7 +1053,8 @@ static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double 
             KernelTimer ts(ctx, "boruvka_scan");
             KernelTimer tr(ctx, round_names[round < 8 ? round : 8]);
             hipLaunchKernelGGL(boruvka_bvh_kernel<D>, dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, st, recs, n,
-                               ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, evals);
+                               ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, round == 0 ? done0 : nullptr,
+                               evals);
         }
         if (evals) {
             unsigned long long h[3];
@@ -964,15 +1075,8 @@ static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double 
         hipLaunchKernelGGL(hook_fix_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, comp_w, comp_key, parent, parent2,
                            ea, eb, ew, n_edges);
         hipLaunchKernelGGL(mark_nonroot_kernel, dim3(g), dim3(256), 0, st, parent2, n, is_root);
-        // pointer jumping to the roots
-        for (int it = 0; it < 64; it++) {
-            int h_changed = 0;
-            HIP_CHECK(hipMemsetAsync(changed, 0, sizeof(int), st));
-            for (int r = 0; r < 4; r++) hipLaunchKernelGGL(jump_kernel, dim3(g), dim3(256), 0, st, parent2, n, changed);
-            HIP_CHECK(hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-            if (!h_changed) break;
-        }
+        // hook trees -> roots (one launch, no host round trip)
+        hipLaunchKernelGGL(resolve_kernel, dim3(g), dim3(256), 0, st, parent2, n);
         hipLaunchKernelGGL(relabel_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, parent2);
         unsigned long long h_ne = 0;
         HIP_CHECK(hipMemcpyAsync(&h_ne, n_edges, 8, hipMemcpyDeviceToHost, st));
@@ -1021,6 +1125,94 @@ void self_edges_device(hdb_ctx *ctx, const double *core, int64_t n, int32_t *va,
     hipLaunchKernelGGL(self_edges_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 256), 4096)), dim3(256), 0,
                        ctx->stream, core, n, va, vb, w);
     HIP_CHECK(hipGetLastError());
+}
+
+
+// ------------------------------------------------- fused exact leaf (a3 + a5)
+// FirstStep's leaf branch for one large partition (FirstStep.java:104-108:
+// calculateCoreDistances then constructMST) on ONE index: K1t also keeps each point's
+// neighbour positions, the core epilogue runs on its lists, and Boruvka's round 0 starts
+// from the kNN seeds (lanes whose seed is provably exact skip the traversal).
+template <int D, int K>
+static void exact_leaf_impl(hdb_ctx *ctx, const double *X, int64_t n, int min_pts, int semantics, double *core,
+                            int self_edges, int32_t *va, int32_t *vb, double *w) {
+    KernelTimer tt(ctx, "exact_leaf_total");
+    auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t bx = rnd(boruvka_extra_bytes(n));
+    const size_t nk = (size_t)n * K;
+    const size_t more = rnd(8 * nk) + rnd(4 * nk) + rnd(8 * nk) + rnd((size_t)n) + 256;
+    Carve cv;
+    char *extra = nullptr;
+    Spatial<D> sp = build_spatial_in<D>(ctx, A_WORK0, X, n, nullptr, cv, bx + more, &extra);
+    Carve ex;
+    ex.base = extra + bx;
+    double *lists = ex.take<double>(nk);
+    int32_t *nb_pos = ex.take<int32_t>(nk);
+    double *nb_s = ex.take<double>(nk);
+    uint8_t *done = ex.take<uint8_t>((size_t)n);
+    unsigned long long *stats = ctx->count_evals ? ex.take<unsigned long long>(3) : nullptr;
+    if (stats) HIP_CHECK(hipMemsetAsync(stats, 0, 24, ctx->stream));
+    {
+        KernelTimer t(ctx, "knn_tree");
+        hipLaunchKernelGGL((knn_tree_kernel<D, K, true>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256), 0,
+                           ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, semantics == HDB_CORE_EXCL_SELF ? 1 : 0, lists,
+                           nb_pos, nb_s, stats);
+        HIP_CHECK(hipGetLastError());
+    }
+    if (stats) {
+        unsigned long long h[3];
+        HIP_CHECK(hipMemcpyAsync(h, stats, 24, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->stats["knn_tree_evals"] = (int64_t)h[0];
+    }
+    core_epilogue_device(ctx, lists, n, K, min_pts - 1, semantics, core);
+    const int g = (int)std::min<int64_t>(ceil_div(n, 256), 4096);
+    hipLaunchKernelGGL(set_core_kernel<D>, dim3(g), dim3(256), 0, ctx->stream, sp.recs, n, core);
+    BoruvkaState<D> bs = boruvka_state<D>(extra, n);
+    hipLaunchKernelGGL((knn_seed_kernel<D, K>), dim3(g), dim3(256), 0, ctx->stream, sp.recs, n, nb_pos, nb_s,
+                       bs.best_w, bs.best_s, bs.best_lo, bs.best_hi, done);
+    HIP_CHECK(hipGetLastError());
+    {
+        KernelTimer tb(ctx, "boruvka_total");
+        boruvka_on_index<D>(ctx, sp, n, extra, true, done, va, vb, w);
+    }
+    if (self_edges) self_edges_device(ctx, core, n, va + (n - 1), vb + (n - 1), w + (n - 1));
+}
+
+template <int D>
+static bool exact_leaf_k(hdb_ctx *ctx, const double *X, int64_t n, int min_pts, int semantics, double *core,
+                         int self_edges, int32_t *va, int32_t *vb, double *w) {
+    switch (pick_kc(min_pts - 1)) {
+    case 1: exact_leaf_impl<D, 1>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); return true;
+    case 3: exact_leaf_impl<D, 3>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); return true;
+    case 7: exact_leaf_impl<D, 7>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); return true;
+    case 15: exact_leaf_impl<D, 15>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); return true;
+    case 31: exact_leaf_impl<D, 31>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); return true;
+    default: return false;
+    }
+}
+
+void exact_leaf_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int min_pts, int metric, int semantics,
+                       double *core, int self_edges, int32_t *va, int32_t *vb, double *w) {
+    if (n <= 0) return;
+    if (min_pts < 1 || min_pts > 32) HDB_THROW(HDB_EINVAL, "minPts must be in 1..32");
+    bool done = false;
+    if (metric == HDB_METRIC_EUCLIDEAN && min_pts >= 2 && n >= 2) {
+        switch (d) {
+        case 1: done = exact_leaf_k<1>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); break;
+        case 2: done = exact_leaf_k<2>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); break;
+        case 3: done = exact_leaf_k<3>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); break;
+        case 4: done = exact_leaf_k<4>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); break;
+        case 8: done = exact_leaf_k<8>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); break;
+        case 16: done = exact_leaf_k<16>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); break;
+        default: break;
+        }
+    }
+    if (done) return;
+    // the two calls on separate indexes (min_pts 1, tiny n, other d)
+    core_distances_device(ctx, X, n, d, min_pts, metric, semantics, core);
+    boruvka_device(ctx, X, n, d, core, metric, va, vb, w);
+    if (self_edges) self_edges_device(ctx, core, n, va + (n - 1), vb + (n - 1), w + (n - 1));
 }
 
 void boruvka_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const double *core, int metric, int32_t *va,

@@ -180,6 +180,23 @@ class HDBSCANStar:
                                         A.ptr(va), A.ptr(vb), A.ptr(w)), "constructMSTBoruvka")
         return UndirectedGraph(va, vb, w)
 
+    def exactMST(self, dataSet, k: int, distanceFunction=None, semantics: int = A.CORE_EXCL_SELF,
+                 selfEdges: bool = True):
+        """FirstStep's leaf branch on one large partition (FirstStep.java:104-108):
+        calculateCoreDistances + the exact MRD MST (constructMSTBoruvka's weights and edge
+        order) in one call sharing one spatial index.  Returns (core, UndirectedGraph)."""
+        X = A.Arr(dataSet, np.float64)
+        n, d = X.obj.shape
+        ne = (n - 1) + (n if selfEdges else 0)
+        core = A.new_like(X, (n,), np.float64)
+        va = A.new_like(X, (ne,), np.int32)
+        vb = A.new_like(X, (ne,), np.int32)
+        w = A.new_like(X, (ne,), np.float64)
+        c = _ctx(X, self.ctx)
+        A.check(A.lib().hdb_exact_mst(c.h, X.p, n, d, k, metric_of(distanceFunction), semantics, int(bool(selfEdges)),
+                                      A.ptr(core), A.ptr(va), A.ptr(vb), A.ptr(w)), "exactMST")
+        return core, UndirectedGraph(va, vb, w)
+
     def knn(self, dataSet, k: int, distanceFunction=None, exclSelf: bool = False, withIndices: bool = False):
         """Per-row k smallest distances (ascending, Double.MAX_VALUE padded) [+ indices]."""
         X = A.Arr(dataSet, np.float64)

@@ -123,6 +123,14 @@ int hdb_leaf_msts(hdb_ctx *ctx, const double *X, const int64_t *offsets, int32_t
  * K2b).  Any MST: the sorted weight sequence equals the reference Prim's exactly; the
  * topology can differ only among equal-weight edges (ties broken by (w, min id, max id)).
  * Outputs n-1 edges (va < vb, by the library's order), then n self edges if self_edges. */
+/* FirstStep's leaf branch for one large partition in one call (FirstStep.java:104-108:
+ * HDBSCANStar.calculateCoreDistances then constructMST): core distances (semantics as
+ * hdb_core_distances, bit-identical) and the exact mutual-reachability MST of
+ * hdb_mst_boruvka (same weights and edge order), sharing one spatial index; the k-NN lists
+ * seed Boruvka's first round.  core_out nullable.  Local vertex ids 0..n-1. */
+int hdb_exact_mst(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t min_pts, int32_t metric,
+                  int32_t semantics, int32_t self_edges, double *core_out, int32_t *va, int32_t *vb, double *w);
+
 int hdb_mst_boruvka(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const double *core, int32_t metric,
                     int32_t self_edges, int32_t *va, int32_t *vb, double *w);
 

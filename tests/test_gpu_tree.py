@@ -133,3 +133,58 @@ def test_tree_full_size_rows(star):
         s = s + (X[r, 2] - X[:, 2]) * (X[r, 2] - X[:, 2])
         s[r] = np.inf
         assert got[r] == np.sqrt(np.partition(s, 2)[:3].max()), r
+
+
+# ------------------------------------------- fused exact leaf (hdb_exact_mst)
+def _sorted_edges(g):
+    return g.getVerticeA(), g.getVericeB(), g.getEges()
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 4, 8, 16])
+@pytest.mark.parametrize("min_pts", [2, 4, 9])
+def test_exact_mst_equals_two_calls(star, oracle, d, min_pts):
+    """hdb_exact_mst (one index, kNN-seeded Boruvka round 0) == calculateCoreDistances +
+    constructMSTBoruvka, bit for bit: cores for all three semantics, and the same edges in
+    the same order (the (w, s, lo, hi) key makes the MST unique)."""
+    X = np.round(blobs(6000, d, 8, 11 * d + min_pts), 1)  # rounded: heavy weight ties
+    for sem in range(3):
+        core, g = star.exactMST(X, min_pts, None, sem, selfEdges=True)
+        ref_core = oracle.core_distances(X, min_pts, semantics=sem)
+        assert eq(core, ref_core), sem
+        b = star.constructMSTBoruvka(X, ref_core, True)
+        for u, v in zip(_sorted_edges(g), _sorted_edges(b)):
+            assert eq(np.asarray(u, dtype=np.float64), np.asarray(v, dtype=np.float64)), (d, sem)
+
+
+def test_exact_mst_weights_equal_prim_skin(star, oracle):
+    """Skin prefix (integer RGB, massive duplication): the sorted MST weights equal the
+    reference Prim's (HDBSCANStar.java:124-205) exactly."""
+    X = load_skin(12000)
+    core, g = star.exactMST(X, 4, None, 2, selfEdges=False)
+    ref_core = oracle.core_distances(X, 4, semantics=2)
+    assert eq(core, ref_core)
+    _, _, w = oracle.prim_mst(X, ref_core, self_edges=False)
+    assert eq(np.sort(g.getEges()), np.sort(w))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 64, 65, 4097])
+def test_exact_mst_ragged(star, oracle, n):
+    X = blobs(n, 3, 3, n + 1)
+    core, g = star.exactMST(X, 4, None, 2, selfEdges=True)
+    assert eq(core, oracle.core_distances(X, 4, semantics=2))
+    assert len(g.getEges()) == 2 * n - 1
+    _, _, w = oracle.prim_mst(X, core, self_edges=False)
+    assert eq(np.sort(g.getEges()[: n - 1]), np.sort(w))
+
+
+def test_exact_mst_device_full_size(star):
+    """1M x 3 (config 2) on device tensors: cores equal the split path, MST equals
+    constructMSTBoruvka edge for edge."""
+    import torch
+    t = torch.from_numpy(blobs(1_000_000, 3, 20, 1)).cuda()
+    core, g = star.exactMST(t, 4, None, 2, selfEdges=False)
+    ref_core = star.calculateCoreDistances(t, 4, None, 2)
+    assert torch.equal(core, ref_core)
+    b = star.constructMSTBoruvka(t, ref_core, False)
+    assert torch.equal(g.getEges(), b.getEges())
+    assert torch.equal(g.getVerticeA(), b.getVerticeA()) and torch.equal(g.getVericeB(), b.getVericeB())
