@@ -60,6 +60,7 @@ struct hdb_ctx {
     bool knn_tree = true;     // K1t (box-pruned) for euclidean lists when the shape allows
     int64_t knn_tree_min_n = 8192;
     bool boruvka_seed = true;
+    bool boruvka_knn_seed = true;  // exact leaf: k-NN lists seed every Boruvka round
     bool prim_coop = true;  // cooperative single-launch Prim for 4096 < n <= 65536  // seed Boruvka rounds from the previous round's edges
     bool count_evals = false;  // K1t counts evaluated pairs (diagnostic; costs one sync)
     std::map<std::string, int64_t> stats;  // diagnostic counters (count_evals)

@@ -235,6 +235,10 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
         ctx->boruvka_seed = value != 0;
         return HDB_OK;
     }
+    if (k == "boruvka_knn_seed") {
+        ctx->boruvka_knn_seed = value != 0;
+        return HDB_OK;
+    }
     if (k == "count_evals") {
         ctx->count_evals = value != 0;
         return HDB_OK;

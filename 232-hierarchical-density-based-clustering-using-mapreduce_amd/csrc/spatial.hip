@@ -31,6 +31,9 @@
 // never prunes a winner: pruning needs LB > bound strictly).
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <vector>
+
 #include "internal.hpp"
 
 namespace hdb {
@@ -46,6 +49,38 @@ struct Rec {
 };
 
 __device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
+
+// A leaf tile staged in LDS: one coalesced vector load (lane l fetches record l of the tile),
+// then every candidate is a broadcast LDS read at a wave-uniform address.  Replaces one
+// dependent scalar load per candidate (the scalar cache serialises a leaf into many round
+// trips); 16-B aligned rows so a record is a few ds_read_b128.
+template <int D>
+struct alignas(16) LRec {
+    double x[D];
+    double core;
+    int32_t comp;
+    int32_t id;
+};
+
+template <int D>
+__device__ __forceinline__ LRec<D> fetch_rec(const Rec<D> *__restrict__ recs, int64_t n, int64_t q) {
+    LRec<D> r;
+    if (q < n) {
+        const Rec<D> g = recs[q];
+#pragma unroll
+        for (int c = 0; c < D; c++) r.x[c] = g.x[c];
+        r.core = g.core;
+        r.comp = g.comp;
+        r.id = g.id;
+    } else {
+#pragma unroll
+        for (int c = 0; c < D; c++) r.x[c] = 0;
+        r.core = 0;
+        r.comp = -5;
+        r.id = -5;
+    }
+    return r;
+}
 
 // ---------------------------------------------------------------- morton
 // bounding box of X: per-block partial min/max over rows (fmin/fmax ignore NaN), then one
@@ -267,14 +302,23 @@ __global__ void bvh_tag_kernel(int32_t *__restrict__ tag, int64_t child_off, int
 
 // lane lower bound (squared) from point x to a box.  Monotone rounding makes it a true
 // lower bound of the computed squared distance of every point in the box (see header).
+// All 2D box values are loaded up front and combined without branches, so a box test is one
+// memory round trip (a conditional form lets the compiler sink each load into its branch:
+// 2D dependent round trips per test).  max(a - x, x - b, 0) equals the gap to [a, b]
+// (x < a: a - x; x > b: x - b; else 0; NaN x or an all-NaN box: 0, i.e. "needed").
 template <int D>
 __device__ __forceinline__ double box_lb2(const double (&x)[D], const double *__restrict__ l,
                                           const double *__restrict__ h) {
+    double a[D], b[D];
+#pragma unroll
+    for (int c = 0; c < D; c++) {
+        a[c] = l[c];
+        b[c] = h[c];
+    }
     double lb = 0;
 #pragma unroll
     for (int c = 0; c < D; c++) {
-        double a = l[c], b = h[c];
-        double g = x[c] < a ? a - x[c] : (x[c] > b ? x[c] - b : 0.0);
+        const double g = fmax(fmax(a[c] - x[c], x[c] - b[c]), 0.0);
         lb = lb + g * g;
     }
     return lb;
@@ -287,25 +331,25 @@ __device__ __forceinline__ void push_children(const Bvh &bvh, int lev, int64_t i
                                               const double *qhi, int32_t *stk, int &sp, int lane, Needs needs) {
     const int64_t c0 = idx * FAN;
     const int64_t c1 = min(c0 + FAN, bvh.cnt[lev - 1]);
+    const int64_t base = bvh.off[lev - 1];
     double key[FAN];
     bool ok[FAN];
+    // straight-line over the FAN children (index clamped, validity masked) so every child's
+    // box and tag load issues before the first test: one round trip per expansion
 #pragma unroll
     for (int k = 0; k < FAN; k++) {
-        ok[k] = false;
-        key[k] = INFINITY;
         const int64_t c = c0 + k;
-        if (c < c1) {
-            const int64_t cn = bvh.off[lev - 1] + c;
-            ok[k] = __any(needs(cn));
-            double kk = 0;
-            const double *cl = bvh.lo + cn * D, *ch = bvh.hi + cn * D;
+        const int64_t cn = base + (c < c1 ? c : c1 - 1);
+        const bool nd = needs(cn);
+        double kk = 0;
+        const double *cl = bvh.lo + cn * D, *ch = bvh.hi + cn * D;
 #pragma unroll
-            for (int d = 0; d < D; d++) {
-                double g = qhi[d] < cl[d] ? cl[d] - qhi[d] : (ch[d] < qlo[d] ? qlo[d] - ch[d] : 0.0);
-                kk = kk + g * g;
-            }
-            key[k] = kk;
+        for (int d = 0; d < D; d++) {
+            const double g = fmax(fmax(cl[d] - qhi[d], qlo[d] - ch[d]), 0.0);
+            kk = kk + g * g;
         }
+        key[k] = kk;
+        ok[k] = (c < c1) && __any(nd);
     }
 #pragma unroll 1
     for (int r = 0; r < FAN; r++) {
@@ -358,9 +402,12 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
                                                           const uint8_t *__restrict__ done,
                                                           unsigned long long *__restrict__ stats) {
     __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
+    __shared__ LRec<D> tile_s[4][BT];
     const int w = threadIdx.x >> 6;
     const int64_t t = (int64_t)blockIdx.x * 4 + w;
     if (t >= ntiles) return;
+    const long long t_start = stats ? clock64() : 0;
+    LRec<D> *cand = tile_s[w];
     const int lane = threadIdx.x & 63;
     int32_t *stk = stack_s[w];
     const int64_t i = t * BT + lane;
@@ -383,6 +430,7 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
     Best b{INFINITY, INFINITY, INT32_MAX, INT32_MAX};
     if (valid && best_w[i] < INFINITY) b = Best{best_w[i], best_s[i], best_lo[i], best_hi[i]};  // seed_kernel
     double cb2 = INFINITY;  // padded square of the component bound
+    double cwv = INFINITY;  // the component bound itself: every lane candidate has w >= mcore
     // squared-distance bound from the lane's own best: a candidate can only win with
     // s <= sb.  b.w == own core: ties need s <= b.s (exact: lb <= s by monotone rounding);
     // otherwise sqrt(s) <= b.w, i.e. s <= b.w^2 (padded: s > fl(b^2)(1+2^-48) proves
@@ -398,16 +446,21 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
             double cwd = __longlong_as_double((long long)cw);
             double c2 = (cwd * cwd) * (1.0 + 1e-12);
             if (c2 < cb2) cb2 = c2;
+            if (cwd < cwv) cwv = cwd;
         }
     };
     auto bound = [&]() -> double { return sb < cb2 ? sb : cb2; };
     const bool search = valid && !(done && done[i]);  // a done lane's seed is its exact best
+    refresh();  // the seeds already bound the component (seed kernels publish before the scan)
+    const bool active0 = search && !(mcore > cwv);
+    // MRD >= own core (HDBSCANStar.java:164-166): a lane whose core exceeds the component
+    // bound cannot supply the component's edge (false for a NaN core, which never raises MRD).
+    // Branch-free so the box loads are not sunk into conditional blocks.
     auto needs_box = [&](const double *lo, const double *hi, int32_t tg) -> bool {
-        if (!search) return false;
-        if (tg >= 0 && tg == mcomp) return false;
+        const double lb = box_lb2<D>(mx, lo, hi);
         const double bd = bound();
-        if (!(bd < INFINITY)) return true;
-        return !(box_lb2<D>(mx, lo, hi) > bd);
+        const bool same = (tg >= 0) & (tg == mcomp);
+        return search & !(mcore > cwv) & !same & (!(bd < INFINITY) | !(lb > bd));
     };
     auto lane_needs = [&](int64_t node) -> bool { return needs_box(bvh.lo + node * D, bvh.hi + node * D, bvh.tag[node]); };
     const double *qlo = bvh.lo + t * D, *qhi = bvh.hi + t * D;
@@ -428,18 +481,34 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
             push_children<D>(bvh, lev, idx, qlo, qhi, stk, sp, lane, lane_needs);
             continue;
         }
-        // leaf: tile idx, 4 groups of 16 candidates
+        // leaf: tile idx, 4 groups of 16 candidates.  The tile's records are fetched with one
+        // vector load while the groups are culled, then staged in LDS.
         n_leaf++;
         bool found = false;
-#pragma unroll 1
+        const LRec<D> mine = fetch_rec<D>(recs, n, idx * BT + lane);
+        bool gneed[NSG];
+        unsigned gmask = 0;
+#pragma unroll
         for (int gi = 0; gi < NSG; gi++) {
             const int64_t sg = idx * NSG + gi;
-            const bool need = needs_box(bvh.slo + sg * D, bvh.shi + sg * D, bvh.stag[sg]);
+            gneed[gi] = needs_box(bvh.slo + sg * D, bvh.shi + sg * D, bvh.stag[sg]);
+            if (__any(gneed[gi])) gmask |= 1u << gi;
+        }
+        if (gmask == 0) continue;
+        __builtin_amdgcn_wave_barrier();
+        cand[lane] = mine;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+        for (int gi = 0; gi < NSG; gi++) {
+            if (!((gmask >> gi) & 1u)) continue;
+            const int64_t sg = idx * NSG + gi;  // re-test: the bound may have tightened
+            const bool need = gneed[gi] && needs_box(bvh.slo + sg * D, bvh.shi + sg * D, bvh.stag[sg]);
             if (!__any(need)) continue;
-            const int64_t j0 = sg * SG, j1 = min(j0 + SG, n);
+            const int q0 = gi * SG;
+            const int q1 = (int)min<int64_t>(SG, n - (idx * BT + q0)) + q0;
 #pragma unroll 4
-            for (int64_t q = j0; q < j1; q++) {
-                const Rec<D> &r = recs[q];  // uniform -> scalar loads
+            for (int qq = q0; qq < q1; qq++) {
+                const LRec<D> r = cand[qq];  // uniform address -> LDS broadcast
                 double s = sq_diff(mx[0], r.x[0]);
 #pragma unroll
                 for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
@@ -465,6 +534,7 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
                 if (bw < __hip_atomic_load(&comp_w[mcomp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                     atomicMin(&comp_w[mcomp], bw);
                 cb2 = c2;
+                if (b.w < cwv) cwv = b.w;
             }
         }
     }
@@ -477,10 +547,14 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
     publish_min(comp_w, mcomp, dbits(b.w), valid && b.w < INFINITY);
     if (stats) {
         for (int off = 32; off >= 1; off >>= 1) nev += __shfl_xor(nev, off);
+        const unsigned long long act_mask = __ballot(active0);
         if (lane == 0) {
             atomicAdd(&stats[0], nev);
             atomicAdd(&stats[1], n_leaf);
             atomicAdd(&stats[2], (unsigned long long)visits);
+            atomicAdd(&stats[3], (unsigned long long)__popcll(act_mask));  // lanes searching at start
+            atomicAdd(&stats[4], (unsigned long long)(act_mask != 0));     // waves with any such lane
+            stats[8 + t] = (unsigned long long)(clock64() - t_start);        // per-wave shader cycles
         }
     }
 }
@@ -645,51 +719,64 @@ __global__ void set_core_kernel(Rec<D> *__restrict__ recs, int64_t n, const doub
     HDB_GRID_STRIDE(i, n) recs[i].core = core[recs[i].id];
 }
 
-// Round-0 Boruvka seed from the K nearest neighbours K1t just found (sorted positions,
-// squared distances): the best (w, s, lo, hi) among them is a valid candidate, and it is
-// provably the lane's exact best when no other point can beat it: every point outside the
-// list has s' >= s_K (the list holds all points with s' < s_K), so its weight is
-// >= LB = max(fl(sqrt(s_K)), core_p); the seed is exact if w < LB, or w == LB and s < s_K.
-// Exact lanes skip the round-0 traversal.
+// Per-round Boruvka seed from the K nearest neighbours K1t found (sorted positions, squared
+// distances).  Every list member in another component is a valid candidate; the lane keeps
+// the smaller key of those and its incoming seed (best_*: INF, or round r-1's best edge that
+// seed_kernel kept), and publishes it to comp_w so the scan starts with a component bound.
+// The seed is provably the lane's exact best when no point outside the list can beat it:
+// every such point has s' >= s_K (the list holds every point with s' < s_K), so its weight
+// is >= LB = max(fl(sqrt(s_K)), core_p); exact if w < LB, or w == LB and s < s_K.  Exact
+// lanes skip the traversal (done[i] = 1).
 template <int D, int K>
 __global__ void knn_seed_kernel(const Rec<D> *__restrict__ recs, int64_t n, const int32_t *__restrict__ nb_pos,
                                 const double *__restrict__ nb_s, double *__restrict__ best_w, double *__restrict__ best_s,
                                 int32_t *__restrict__ best_lo, int32_t *__restrict__ best_hi,
-                                uint8_t *__restrict__ done) {
-    HDB_GRID_STRIDE(i, n) {
-        const double mcore = recs[i].core;
-        const int32_t mid = recs[i].id;
+                                uint8_t *__restrict__ done, unsigned long long *__restrict__ comp_w) {
+    const int64_t stride = (int64_t)blockDim.x * gridDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {  // wave-uniform trip count
+        const int64_t i = base + threadIdx.x;
+        bool act = false;
+        int32_t mcomp = 0;
         Best b{INFINITY, INFINITY, INT32_MAX, INT32_MAX};
-        double sK = -INFINITY;
-        bool full = true;
-        for (int k = 0; k < K; k++) {
-            const int32_t j = nb_pos[i * K + k];
-            const double s = nb_s[i * K + k];
-            if (j < 0 || !(s < INFINITY)) {
-                full = false;
-                continue;
+        if (i < n) {
+            const Rec<D> &me = recs[i];
+            const double mcore = me.core;
+            const int32_t mid = me.id;
+            mcomp = me.comp;
+            if (best_w[i] < INFINITY) b = Best{best_w[i], best_s[i], best_lo[i], best_hi[i]};
+            double sK = -INFINITY;
+            bool full = true;
+            for (int k = 0; k < K; k++) {
+                const int32_t j = nb_pos[i * K + k];
+                const double s = nb_s[i * K + k];
+                if (j < 0 || !(s < INFINITY)) {
+                    full = false;
+                    continue;
+                }
+                sK = s > sK ? s : sK;
+                if (recs[j].comp == mcomp) continue;  // also the point itself (INCL lists)
+                double mrd = sqrt(s);  // HDBSCANStar.java:162-168 order, as the scan kernel
+                if (mcore > mrd) mrd = mcore;
+                const double oc = recs[j].core;
+                if (oc > mrd) mrd = oc;
+                const int32_t oid = recs[j].id;
+                const int32_t lo = mid < oid ? mid : oid, hi = mid < oid ? oid : mid;
+                if (key_less(mrd, s, lo, hi, b)) b = Best{mrd, s, lo, hi};
             }
-            sK = s > sK ? s : sK;
-            if (j == (int32_t)i) continue;  // INCL lists hold the point itself
-            double mrd = sqrt(s);  // HDBSCANStar.java:162-168 order, as the scan kernel
-            if (mcore > mrd) mrd = mcore;
-            const double oc = recs[j].core;
-            if (oc > mrd) mrd = oc;
-            const int32_t oid = recs[j].id;
-            const int32_t lo = mid < oid ? mid : oid, hi = mid < oid ? oid : mid;
-            if (key_less(mrd, s, lo, hi, b)) b = Best{mrd, s, lo, hi};
+            bool exact = false;
+            if (full && b.w < INFINITY) {
+                double lb = sqrt(sK);
+                if (mcore > lb) lb = mcore;
+                exact = (b.w < lb) || (b.w == lb && b.s < sK);
+            }
+            best_w[i] = b.w;
+            best_s[i] = b.s;
+            best_lo[i] = b.lo;
+            best_hi[i] = b.hi;
+            done[i] = exact ? 1 : 0;
+            act = b.w < INFINITY;
         }
-        bool exact = false;
-        if (full && b.w < INFINITY) {
-            double lb = sqrt(sK);
-            if (mcore > lb) lb = mcore;
-            exact = (b.w < lb) || (b.w == lb && b.s < sK);
-        }
-        best_w[i] = b.w;
-        best_s[i] = b.s;
-        best_lo[i] = b.lo;
-        best_hi[i] = b.hi;
-        done[i] = exact ? 1 : 0;
+        publish_min(comp_w, mcomp, dbits(b.w), act);
     }
 }
 
@@ -697,19 +784,22 @@ __global__ void knn_seed_kernel(const Rec<D> *__restrict__ recs, int64_t n, cons
 // A wave owns query tile t (lane = point).  Its own tile is scanned first (it holds the
 // nearest candidates in Morton order, so the K-th bound is tight from the start), then the
 // BVH is walked nearest-first, skipping any node whose box no lane can still improve on.
-// Candidates are wave-uniform (scalar loads); each lane evaluates the exact FP64 squared
-// distance in the reference's order and feeds the register top-K network.
+// A visited tile is fetched with one vector load and staged in LDS; candidates are then
+// wave-uniform broadcast reads, and each lane evaluates the exact FP64 squared distance in
+// the reference's order and feeds the register top-K network.
 template <int D, int K, bool IDX>
 __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
                                                        Bvh bvh, int excl, double *__restrict__ lists,
                                                        int32_t *__restrict__ nb_pos, double *__restrict__ nb_s,
                                                        unsigned long long *__restrict__ stats) {
     __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
+    __shared__ LRec<D> tile_s[4][BT];
     const int w = threadIdx.x >> 6;
     const int64_t t = (int64_t)blockIdx.x * 4 + w;
     if (t >= ntiles) return;
     const int lane = threadIdx.x & 63;
     int32_t *stk = stack_s[w];
+    LRec<D> *cand = tile_s[w];
     const int64_t i = t * BT + lane;
     const bool valid = i < n;
     double mx[D];
@@ -734,25 +824,33 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
     unsigned long long nev = 0, n_leaf = 0, n_node = 0;
 
     auto needs_box = [&](const double *lo, const double *hi) -> bool {
-        return valid && box_lb2<D>(mx, lo, hi) < buf[K - 1];
+        const double lb = box_lb2<D>(mx, lo, hi);  // loads first: one round trip per test
+        return valid & (lb < buf[K - 1]);
     };
     auto lane_needs = [&](int64_t node) -> bool { return needs_box(bvh.lo + node * D, bvh.hi + node * D); };
     auto scan_leaf = [&](int64_t tile, bool own) {
         n_leaf++;
+        // the tile's 64 records: one coalesced vector load, staged in LDS (broadcast reads)
+        const LRec<D> mine = fetch_rec<D>(recs, n, tile * BT + lane);
+        __builtin_amdgcn_wave_barrier();
+        cand[lane] = mine;
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
         for (int gi = 0; gi < NSG; gi++) {
             const int64_t sg = tile * NSG + gi;
             if (!own && !__any(needs_box(bvh.slo + sg * D, bvh.shi + sg * D))) continue;
             const int64_t j0 = sg * SG, j1 = min(j0 + SG, n);
+            if (j1 <= j0) break;
             nev += (unsigned long long)(j1 - j0);
+            const int q0 = gi * SG, q1 = q0 + (int)(j1 - j0);
 #pragma unroll 4
-            for (int64_t q = j0; q < j1; q++) {
-                const Rec<D> &r = recs[q];  // uniform -> scalar loads
+            for (int qq = q0; qq < q1; qq++) {
+                const LRec<D> r = cand[qq];  // uniform address -> LDS broadcast
                 double s = sq_diff(mx[0], r.x[0]);
 #pragma unroll
                 for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
                 if (r.id == skip_self) s = INFINITY;
-                if (IDX) topk_insert_idx<K>(buf, bix, s, (int)q);
+                if (IDX) topk_insert_idx<K>(buf, bix, s, (int)(tile * BT + qq));
                 else topk_insert<K>(buf, s);
             }
         }
@@ -959,15 +1057,23 @@ bool knn_tree_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC, bo
 static size_t boruvka_extra_bytes(int64_t n) {
     const size_t per = (size_t)n;
     auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
-    return 5 * rnd(8 * per) + 5 * rnd(4 * per) + 3 * 256 + 2 * rnd(4 * per) + rnd(8 * per) + 256;
+    return 5 * rnd(8 * per) + 5 * rnd(4 * per) + 3 * 256 + 2 * rnd(4 * per) + rnd(8 * per) +
+           rnd(8 * (per / 64 + 9));  // + diagnostics: counters and per-wave cycles (count_evals)
 }
 
+// k-NN lists over the index's sorted positions (K1t with IDX): seed every Boruvka round
+struct KnnLists {
+    const int32_t *pos = nullptr;
+    const double *s = nullptr;  // squared distances, ascending per row
+    int K = 0;
+    uint8_t *done = nullptr;  // n flags: the lane's seed is exact this round
+};
+
 // Boruvka rounds over a built index whose records carry the core distances.  extra: the
-// boruvka_extra_bytes(n) region.  seeded: best_* (first 8n/4n arrays of extra) already hold
-// round-0 seeds (done0: lanes whose seed is exact skip the round-0 traversal).
+// boruvka_extra_bytes(n) region.  kl (nullable): k-NN lists that seed every round.
 template <int D>
-static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extra, bool seeded,
-                             const uint8_t *done0, int32_t *va, int32_t *vb, double *w);
+static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extra, const KnnLists *kl,
+                             int32_t *va, int32_t *vb, double *w);
 
 template <int D>
 struct BoruvkaState {
@@ -999,12 +1105,12 @@ static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double 
     char *extra = nullptr;
     KernelTimer tt(ctx, "boruvka_total");
     Spatial<D> sp = build_spatial_in<D>(ctx, A_WORK0, X, n, core, cv, boruvka_extra_bytes(n), &extra);
-    boruvka_on_index<D>(ctx, sp, n, extra, false, nullptr, va, vb, w);
+    boruvka_on_index<D>(ctx, sp, n, extra, nullptr, va, vb, w);
 }
 
 template <int D>
-static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extra, bool seeded,
-                             const uint8_t *done0, int32_t *va, int32_t *vb, double *w) {
+static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extra, const KnnLists *kl,
+                             int32_t *va, int32_t *vb, double *w) {
     const size_t per = (size_t)n;
     size_t used = 0;
     BoruvkaState<D> bs = boruvka_state<D>(extra, n, &used);
@@ -1018,7 +1124,8 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
     unsigned long long *n_edges = ex.take<unsigned long long>(1);
     int32_t *ea = ex.take<int32_t>(per), *eb = ex.take<int32_t>(per);
     double *ew = ex.take<double>(per);
-    unsigned long long *evals = ctx->count_evals ? ex.take<unsigned long long>(3) : nullptr;
+    unsigned long long *evals = ctx->count_evals ? ex.take<unsigned long long>(8 + sp.ntiles) : nullptr;
+    std::vector<unsigned long long> wave_cyc(ctx->count_evals ? sp.ntiles : 0);
     int64_t tot_evals = 0;
     Rec<D> *recs = sp.recs;
     int32_t *inv = sp.inv;
@@ -1028,8 +1135,27 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
     const int g = (int)std::min<int64_t>(ceil_div(n, 256), 4096);
     hipStream_t st = ctx->stream;
     HIP_CHECK(hipMemsetAsync(n_edges, 0, 8, st));
-    if (!seeded) hipLaunchKernelGGL(fill_inf_kernel, dim3(g), dim3(256), 0, st, best_w, n);
+    hipLaunchKernelGGL(fill_inf_kernel, dim3(g), dim3(256), 0, st, best_w, n);
     HIP_CHECK(hipGetLastError());
+    auto knn_seed = [&]() {
+        if (!kl) return;
+        const int gs = (int)std::min<int64_t>(ceil_div(n, 256), 2048);
+#define KNN_SEED(KK)                                                                                                   \
+    case KK:                                                                                                           \
+        hipLaunchKernelGGL((knn_seed_kernel<D, KK>), dim3(gs), dim3(256), 0, st, recs, n, kl->pos, kl->s, best_w,     \
+                           best_s, best_lo, best_hi, kl->done, comp_w);                                                \
+        break;
+        switch (kl->K) {
+            KNN_SEED(1)
+            KNN_SEED(3)
+            KNN_SEED(7)
+            KNN_SEED(15)
+            KNN_SEED(31)
+        default: HDB_THROW(HDB_EINVAL, "knn seed: unsupported list length");
+        }
+#undef KNN_SEED
+        HIP_CHECK(hipGetLastError());
+    };
 
     static const char *round_names[] = {"boruvka_r0", "boruvka_r1", "boruvka_r2", "boruvka_r3", "boruvka_r4",
                                         "boruvka_r5", "boruvka_r6", "boruvka_r7", "boruvka_r8+"};
@@ -1043,24 +1169,35 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
         HIP_CHECK(hipMemsetAsync(comp_w, 0xff, 8 * n, st));
         HIP_CHECK(hipMemsetAsync(comp_key, 0xff, 8 * n, st));
         HIP_CHECK(hipMemsetAsync(comp_s, 0xff, 8 * n, st));
-        if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 24, st));
+        if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 40, st));
         if (round > 0 && ctx->boruvka_seed)
             hipLaunchKernelGGL(seed_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, inv, best_w, best_lo, best_hi,
                                comp_w);
         else if (round > 0)
             hipLaunchKernelGGL(fill_inf_kernel, dim3(g), dim3(256), 0, st, best_w, n);
+        knn_seed();
         {
             KernelTimer ts(ctx, "boruvka_scan");
             KernelTimer tr(ctx, round_names[round < 8 ? round : 8]);
             hipLaunchKernelGGL(boruvka_bvh_kernel<D>, dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, st, recs, n,
-                               ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, round == 0 ? done0 : nullptr,
-                               evals);
+                               ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, kl ? kl->done : nullptr, evals);
         }
         if (evals) {
-            unsigned long long h[3];
-            HIP_CHECK(hipMemcpyAsync(h, evals, 24, hipMemcpyDeviceToHost, st));
+            unsigned long long h[5];
+            HIP_CHECK(hipMemcpyAsync(h, evals, 40, hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
             const std::string r = "boruvka_r" + std::to_string(round);
+            HIP_CHECK(hipMemcpyAsync(wave_cyc.data(), evals + 8, 8 * sp.ntiles, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            std::sort(wave_cyc.begin(), wave_cyc.end());
+            unsigned long long cs = 0;
+            for (auto c : wave_cyc) cs += c;
+            ctx->stats[r + "_wave_cyc_mean"] = (int64_t)(cs / wave_cyc.size());
+            ctx->stats[r + "_wave_cyc_p50"] = (int64_t)wave_cyc[wave_cyc.size() / 2];
+            ctx->stats[r + "_wave_cyc_p99"] = (int64_t)wave_cyc[wave_cyc.size() * 99 / 100];
+            ctx->stats[r + "_wave_cyc_max"] = (int64_t)wave_cyc.back();
+            ctx->stats[r + "_active_lanes"] = (int64_t)h[3];
+            ctx->stats[r + "_active_waves"] = (int64_t)h[4];
             ctx->stats[r + "_evals"] = (int64_t)h[0];
             ctx->stats[r + "_leaves"] = (int64_t)h[1];
             ctx->stats[r + "_nodes"] = (int64_t)h[2];
@@ -1168,13 +1305,14 @@ static void exact_leaf_impl(hdb_ctx *ctx, const double *X, int64_t n, int min_pt
     core_epilogue_device(ctx, lists, n, K, min_pts - 1, semantics, core);
     const int g = (int)std::min<int64_t>(ceil_div(n, 256), 4096);
     hipLaunchKernelGGL(set_core_kernel<D>, dim3(g), dim3(256), 0, ctx->stream, sp.recs, n, core);
-    BoruvkaState<D> bs = boruvka_state<D>(extra, n);
-    hipLaunchKernelGGL((knn_seed_kernel<D, K>), dim3(g), dim3(256), 0, ctx->stream, sp.recs, n, nb_pos, nb_s,
-                       bs.best_w, bs.best_s, bs.best_lo, bs.best_hi, done);
-    HIP_CHECK(hipGetLastError());
+    KnnLists kl;
+    kl.pos = nb_pos;
+    kl.s = nb_s;
+    kl.K = K;
+    kl.done = done;
     {
         KernelTimer tb(ctx, "boruvka_total");
-        boruvka_on_index<D>(ctx, sp, n, extra, true, done, va, vb, w);
+        boruvka_on_index<D>(ctx, sp, n, extra, ctx->boruvka_knn_seed ? &kl : nullptr, va, vb, w);
     }
     if (self_edges) self_edges_device(ctx, core, n, va + (n - 1), vb + (n - 1), w + (n - 1));
 }

@@ -172,12 +172,13 @@ def main():
     achieved = flops_per_launch / avg_s / 1e12 if avg_s > 0 else 0.0
     algo_flops = 3 * D * (n * n if dom == "knn_tree" else n * (n - 1) / 2) / max(k_n / args.steps, 1)
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_bytes.json")
+    # HBM bytes per launch from the committed rocprofv3 PMC passes (tools/profile_bench.sh,
+    # FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), keyed by kernel symbol
+    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    sym = {"knn_tree": "knn_tree_kernel", "boruvka_scan": "boruvka_bvh_kernel"}[dom]
     if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+        with open(pmc) as fh:
+            traffic = json.load(fh).get(sym, {}).get("hbm_bytes_per_launch")
     line = {
         "metric": "points/sec end-to-end + mutual-reach distance evals/sec at 1/2/4/8 GPUs",
         "value": value,

@@ -73,6 +73,11 @@ int hdb_ctx_synchronize(hdb_ctx *ctx);
  *                                  (default 8192) and d in {1,2,3,4,8,16} use K1t, the
  *                                  box-pruned traversal of the Morton/BVH index, instead of
  *                                  the all-pairs K1;
+ *   "prim_coop"       (default 1): single-launch cooperative Prim for 4096 < n <= 65536;
+ *   "boruvka_seed"    (default 1): a Boruvka round starts from the previous round's still
+ *                                  valid per-point edges;
+ *   "boruvka_knn_seed"(default 1): hdb_exact_mst seeds every Boruvka round from the k-NN
+ *                                  lists (lanes whose seed is provably exact skip the scan);
  *   "count_evals"     (default 0): K1t counts the pairs it evaluates (read "last_evals"). */
 int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value);
 /* Diagnostic counters: "last_evals" = pair evaluations of the last K1t call (count_evals on). */
@@ -123,16 +128,16 @@ int hdb_leaf_msts(hdb_ctx *ctx, const double *X, const int64_t *offsets, int32_t
  * K2b).  Any MST: the sorted weight sequence equals the reference Prim's exactly; the
  * topology can differ only among equal-weight edges (ties broken by (w, min id, max id)).
  * Outputs n-1 edges (va < vb, by the library's order), then n self edges if self_edges. */
+int hdb_mst_boruvka(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const double *core, int32_t metric,
+                    int32_t self_edges, int32_t *va, int32_t *vb, double *w);
+
 /* FirstStep's leaf branch for one large partition in one call (FirstStep.java:104-108:
  * HDBSCANStar.calculateCoreDistances then constructMST): core distances (semantics as
  * hdb_core_distances, bit-identical) and the exact mutual-reachability MST of
  * hdb_mst_boruvka (same weights and edge order), sharing one spatial index; the k-NN lists
- * seed Boruvka's first round.  core_out nullable.  Local vertex ids 0..n-1. */
+ * seed every Boruvka round.  core_out nullable.  Local vertex ids 0..n-1. */
 int hdb_exact_mst(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t min_pts, int32_t metric,
                   int32_t semantics, int32_t self_edges, double *core_out, int32_t *va, int32_t *vb, double *w);
-
-int hdb_mst_boruvka(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const double *core, int32_t metric,
-                    int32_t self_edges, int32_t *va, int32_t *vb, double *w);
 
 /* ---------------------------------------------------------- nearest sample (a8, a9)
  * FirstStep.call non-leaf branch (FirstStep.java:74-85): the FIRST minimum over the sample
