@@ -59,9 +59,11 @@ struct hdb_ctx {
     bool force_fp64 = false;  // disable the FP32 screen in K1 (A/B and tests)
     bool knn_tree = true;     // K1t (box-pruned) for euclidean lists when the shape allows
     int64_t knn_tree_min_n = 8192;
-    bool boruvka_seed = true;
+    bool boruvka_seed = true;      // seed Boruvka rounds from the previous round's edges
     bool boruvka_knn_seed = true;  // exact leaf: k-NN lists seed every Boruvka round
-    bool prim_coop = true;  // cooperative single-launch Prim for 4096 < n <= 65536  // seed Boruvka rounds from the previous round's edges
+    int boruvka_wave_pts = 64;     // points per scan wave (16/32/64), compacted per 512-position group
+    int trav_pop_test = 0;         // bit 0: Boruvka re-tests a popped node, bit 1: K1t a popped leaf
+    bool prim_coop = true;         // cooperative single-launch Prim for 4096 < n <= 65536
     bool count_evals = false;  // K1t counts evaluated pairs (diagnostic; costs one sync)
     std::map<std::string, int64_t> stats;  // diagnostic counters (count_evals)
 };

@@ -235,6 +235,14 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
         ctx->boruvka_seed = value != 0;
         return HDB_OK;
     }
+    if (k == "trav_pop_test") {
+        ctx->trav_pop_test = (int)value;
+        return HDB_OK;
+    }
+    if (k == "boruvka_wave_pts") {
+        ctx->boruvka_wave_pts = (int)value;
+        return HDB_OK;
+    }
     if (k == "boruvka_knn_seed") {
         ctx->boruvka_knn_seed = value != 0;
         return HDB_OK;

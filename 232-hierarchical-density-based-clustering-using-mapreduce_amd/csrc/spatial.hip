@@ -39,6 +39,9 @@
 namespace hdb {
 
 constexpr int BT = 64;  // tile size (one wave)
+#ifndef CAND_UNROLL
+#define CAND_UNROLL 2  // candidate-loop unroll: LDS-broadcast latency vs VGPRs (occupancy)
+#endif
 
 template <int D>
 struct Rec {
@@ -324,51 +327,125 @@ __device__ __forceinline__ double box_lb2(const double (&x)[D], const double *__
     return lb;
 }
 
-// Pushes the children of internal node (lev, idx) that some lane needs, farthest first
-// (so the nearest is popped first), ordered by box-to-box distance from the query tile.
-template <int D, class Needs>
-__device__ __forceinline__ void push_children(const Bvh &bvh, int lev, int64_t idx, const double *qlo,
-                                              const double *qhi, int32_t *stk, int &sp, int lane, Needs needs) {
-    const int64_t c0 = idx * FAN;
-    const int64_t c1 = min(c0 + FAN, bvh.cnt[lev - 1]);
-    const int64_t base = bvh.off[lev - 1];
-    double key[FAN];
-    bool ok[FAN];
-    // straight-line over the FAN children (index clamped, validity masked) so every child's
-    // box and tag load issues before the first test: one round trip per expansion
+// the same bound on boxes already in registers
+template <int D>
+__device__ __forceinline__ double box_lb2v(const double (&x)[D], const double (&a)[D], const double (&b)[D]) {
+    double lb = 0;
 #pragma unroll
-    for (int k = 0; k < FAN; k++) {
-        const int64_t c = c0 + k;
-        const int64_t cn = base + (c < c1 ? c : c1 - 1);
-        const bool nd = needs(cn);
+    for (int c = 0; c < D; c++) {
+        const double g = fmax(fmax(a[c] - x[c], x[c] - b[c]), 0.0);
+        lb = lb + g * g;
+    }
+    return lb;
+}
+
+// Cooperative box staging: a run of NB consecutive boxes (lo/hi rows of D doubles, plus tags)
+// is fetched with lanes loading DIFFERENT elements -- one round trip, one or two VGPRs per
+// lane -- and parked in the wave's LDS area; the tests then read each box back with
+// broadcast LDS reads.  (Every lane loading every box at a uniform address would hold
+// NB x 2D doubles in VGPRs per lane and cut occupancy to ~3 waves/SIMD.)  Boxes past
+// nvalid become empty (+inf, -inf; tag -1), so their lower bound is +inf.
+constexpr int BOXBUF = 2 * FAN;  // doubles per dimension in the per-wave staging area
+template <int D, int NB>
+__device__ __forceinline__ void stage_boxes(const double *__restrict__ lo, const double *__restrict__ hi,
+                                            const int32_t *__restrict__ tag, int nvalid, double *sb, int32_t *st,
+                                            int lane) {
+    constexpr int E = NB * D, R = (E + 63) / 64;
+    double l[R], h[R];
+    const int last = nvalid * D - 1;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int e = lane + 64 * r;
+        const int ec = e < last ? e : last;  // clamped: unconditional, in-bounds loads
+        l[r] = lo[ec];
+        h[r] = hi[ec];
+    }
+    int32_t tg = tag[lane < nvalid - 1 ? lane : nvalid - 1];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int e = lane + 64 * r;
+        if (e < E) {
+            const bool ok = e / D < nvalid;
+            sb[e] = ok ? l[r] : INFINITY;
+            sb[E + e] = ok ? h[r] : -INFINITY;
+        }
+    }
+    if (lane < NB) st[lane] = lane < nvalid ? tg : -1;
+    __builtin_amdgcn_wave_barrier();
+}
+template <int D, int NB>
+__device__ __forceinline__ void staged_box(const double *sb, int k, double (&a)[D], double (&b)[D]) {
+#pragma unroll
+    for (int c = 0; c < D; c++) {
+        a[c] = sb[k * D + c];
+        b[c] = sb[NB * D + k * D + c];
+    }
+}
+
+// The BVH level table (offset and node count per level, as bvh_shape) rebuilt per wave in
+// LDS from ntiles: reading Bvh::off/cnt with a dynamic level index from the kernel arguments
+// keeps both arrays resident in SGPRs and spills them to VGPR lanes.
+__device__ __forceinline__ void level_table(int64_t ntiles, int64_t *off_s, int64_t *cnt_s, int lane) {
+    if (lane <= MAXLEV) {
+        int64_t c = ntiles, o = 0;
+        for (int l = 0; l < lane; l++) {
+            o += c;
+            c = (c + FAN - 1) / FAN;
+        }
+        off_s[lane] = o;
+        cnt_s[lane] = c;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Pushes the children of internal node (lev, idx) that some lane needs, farthest first
+// (so the nearest is popped first), ordered by box-to-box distance from the query box.
+// needs(a, b, tag): does this lane need the box [a, b] with that tag.  The per-child test
+// loop is not unrolled (one child's box live at a time: low VGPR count, high occupancy);
+// the ordering is lane-parallel: lane k < FAN ranks child k among the needed children and
+// writes its stack slot directly.
+template <int D, class Needs>
+__device__ __forceinline__ void push_children(const Bvh &bvh, const int64_t *off_s, const int64_t *cnt_s, int lev,
+                                              int64_t idx, const double *qlo, const double *qhi, int32_t *stk,
+                                              int &sp, int lane, double *sb, int32_t *st, Needs needs) {
+    const int64_t c0 = idx * FAN;
+    const int64_t c1 = min(c0 + FAN, cnt_s[lev - 1]);
+    const int64_t base = off_s[lev - 1] + c0;
+    const int nc = (int)(c1 - c0);
+    stage_boxes<D, FAN>(bvh.lo + base * D, bvh.hi + base * D, bvh.tag + base, nc, sb, st, lane);
+    unsigned okmask = 0;
+#pragma unroll 1
+    for (int k = 0; k < nc; k++) {
+        double a[D], b[D];
+        staged_box<D, FAN>(sb, k, a, b);
+        if (__any(needs(a, b, st[k]))) okmask |= 1u << k;
+    }
+    okmask = __builtin_amdgcn_readfirstlane(okmask);
+    if (okmask == 0) return;
+    // lane k: key of child k (box-to-box squared gap), then its rank among needed children
+    double key = -1.0;
+    const bool mine = lane < FAN && ((okmask >> lane) & 1u);
+    if (mine) {
         double kk = 0;
-        const double *cl = bvh.lo + cn * D, *ch = bvh.hi + cn * D;
 #pragma unroll
         for (int d = 0; d < D; d++) {
-            const double g = fmax(fmax(cl[d] - qhi[d], qlo[d] - ch[d]), 0.0);
+            const double g = fmax(fmax(sb[lane * D + d] - qhi[d], qlo[d] - sb[FAN * D + lane * D + d]), 0.0);
             kk = kk + g * g;
         }
-        key[k] = kk;
-        ok[k] = (c < c1) && __any(nd);
+        key = kk;
     }
-#pragma unroll 1
-    for (int r = 0; r < FAN; r++) {
-        int sel = -1;
-        double sk = -1.0;
+    int rank = 0;
 #pragma unroll
-        for (int k = 0; k < FAN; k++)
-            if (ok[k] && key[k] > sk) {
-                sk = key[k];
-                sel = k;
-            }
-        sel = __builtin_amdgcn_readfirstlane(sel);
-        if (sel < 0) break;
-#pragma unroll
-        for (int k = 0; k < FAN; k++)
-            if (k == sel) ok[k] = false;
-        if (lane == 0) stk[sp] = ((lev - 1) << 26) | (int32_t)(c0 + sel);
-        sp++;
+    for (int j = 0; j < FAN; j++) {
+        const double kj = __shfl(key, j);
+        const bool okj = (okmask >> j) & 1u;
+        rank += (okj && (kj > key || (kj == key && j < lane))) ? 1 : 0;
     }
+    __builtin_amdgcn_wave_barrier();
+    if (mine) stk[sp + rank] = ((lev - 1) << 26) | (int32_t)(c0 + lane);
+    __builtin_amdgcn_wave_barrier();
+    sp += __popc(okmask);
 }
 
 // Publishes min(v) per component into arr with few atomics: late rounds put most of the
@@ -399,19 +476,30 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
                                                           Bvh bvh, unsigned long long *__restrict__ comp_w,
                                                           double *__restrict__ best_w, double *__restrict__ best_s,
                                                           int32_t *__restrict__ best_lo, int32_t *__restrict__ best_hi,
-                                                          const uint8_t *__restrict__ done,
+                                                          const int32_t *__restrict__ work,
+                                                          const unsigned long long *__restrict__ desc,
+                                                          const int32_t *__restrict__ nwaves, int pop_test,
                                                           unsigned long long *__restrict__ stats) {
     __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
     __shared__ LRec<D> tile_s[4][BT];
+    __shared__ double boxs_s[4][BOXBUF * D];
+    __shared__ int32_t boxt_s[4][FAN];
+    __shared__ int64_t lvl_s[4][2 * (MAXLEV + 1)];
     const int w = threadIdx.x >> 6;
+    double *bxs = boxs_s[w];
+    int32_t *bxt = boxt_s[w];
+    int64_t *off_s = lvl_s[w], *cnt_s = lvl_s[w] + MAXLEV + 1;
     const int64_t t = (int64_t)blockIdx.x * 4 + w;
-    if (t >= ntiles) return;
+    // compacted work list (group_compact_kernel): wave t takes desc[t]'s run of sorted
+    // positions; the grid covers the worst case, waves past the count exit
+    if (t >= *nwaves) return;
     const long long t_start = stats ? clock64() : 0;
     LRec<D> *cand = tile_s[w];
     const int lane = threadIdx.x & 63;
     int32_t *stk = stack_s[w];
-    const int64_t i = t * BT + lane;
-    const bool valid = i < n;
+    const unsigned long long dsc = desc[t];
+    const bool valid = lane < (int)(dsc & 255u);
+    const int64_t i = valid ? work[(int64_t)(dsc >> 8) + lane] : 0;
     unsigned long long n_leaf = 0, nev = 0;
     double mx[D];
     double mcore = 0;
@@ -450,20 +538,31 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
         }
     };
     auto bound = [&]() -> double { return sb < cb2 ? sb : cb2; };
-    const bool search = valid && !(done && done[i]);  // a done lane's seed is its exact best
+    const bool search = valid;  // done / dead lanes are not in the work list
     refresh();  // the seeds already bound the component (seed kernels publish before the scan)
     const bool active0 = search && !(mcore > cwv);
     // MRD >= own core (HDBSCANStar.java:164-166): a lane whose core exceeds the component
     // bound cannot supply the component's edge (false for a NaN core, which never raises MRD).
     // Branch-free so the box loads are not sunk into conditional blocks.
-    auto needs_box = [&](const double *lo, const double *hi, int32_t tg) -> bool {
-        const double lb = box_lb2<D>(mx, lo, hi);
+    auto needs_vals = [&](const double (&a)[D], const double (&b)[D], int32_t tg) -> bool {
+        const double lb = box_lb2v<D>(mx, a, b);
         const double bd = bound();
         const bool same = (tg >= 0) & (tg == mcomp);
         return search & !(mcore > cwv) & !same & (!(bd < INFINITY) | !(lb > bd));
     };
-    auto lane_needs = [&](int64_t node) -> bool { return needs_box(bvh.lo + node * D, bvh.hi + node * D, bvh.tag[node]); };
-    const double *qlo = bvh.lo + t * D, *qhi = bvh.hi + t * D;
+    // query box = the wave's own points (orders the children nearest-first)
+    double qlo[D], qhi[D];
+#pragma unroll
+    for (int c = 0; c < D; c++) {
+        double l = valid ? mx[c] : INFINITY, h = valid ? mx[c] : -INFINITY;
+        for (int off = 32; off >= 1; off >>= 1) {
+            l = fmin(l, __shfl_xor(l, off));
+            h = fmax(h, __shfl_xor(h, off));
+        }
+        qlo[c] = l;
+        qhi[c] = h;
+    }
+    level_table(ntiles, off_s, cnt_s, lane);
     int sp = 0;
     if (lane == 0) stk[0] = ((bvh.levels - 1) << 26) | 0;
     sp = 1;
@@ -474,26 +573,35 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
         sp--;
         const int lev = code >> 26;
         const int64_t idx = code & ((1 << 26) - 1);
-        const int64_t node = bvh.off[lev] + idx;
+        const int64_t node = off_s[lev] + idx;
         if ((visits++ & 7) == 0) refresh();
-        if (!__any(lane_needs(node))) continue;
+        // re-test the popped node with the current bound (its parent tested it when pushing)
+        if (pop_test & 1) {
+            stage_boxes<D, 1>(bvh.lo + node * D, bvh.hi + node * D, bvh.tag + node, 1, bxs, bxt, lane);
+            double a[D], bb[D];
+            staged_box<D, 1>(bxs, 0, a, bb);
+            if (!__any(needs_vals(a, bb, bxt[0]))) continue;
+        }
         if (lev > 0) {
-            push_children<D>(bvh, lev, idx, qlo, qhi, stk, sp, lane, lane_needs);
+            push_children<D>(bvh, off_s, cnt_s, lev, idx, qlo, qhi, stk, sp, lane, bxs, bxt, needs_vals);
             continue;
         }
         // leaf: tile idx, 4 groups of 16 candidates.  The tile's records are fetched with one
-        // vector load while the groups are culled, then staged in LDS.
+        // vector load together with the group boxes, then staged in LDS.
         n_leaf++;
         bool found = false;
         const LRec<D> mine = fetch_rec<D>(recs, n, idx * BT + lane);
-        bool gneed[NSG];
+        stage_boxes<D, NSG>(bvh.slo + idx * NSG * D, bvh.shi + idx * NSG * D, bvh.stag + idx * NSG, NSG, bxs, bxt,
+                            lane);
+        auto gneeds = [&](int gi) -> bool {
+            double a[D], bb[D];
+            staged_box<D, NSG>(bxs, gi, a, bb);
+            return needs_vals(a, bb, bxt[gi]);
+        };
         unsigned gmask = 0;
-#pragma unroll
-        for (int gi = 0; gi < NSG; gi++) {
-            const int64_t sg = idx * NSG + gi;
-            gneed[gi] = needs_box(bvh.slo + sg * D, bvh.shi + sg * D, bvh.stag[sg]);
-            if (__any(gneed[gi])) gmask |= 1u << gi;
-        }
+#pragma unroll 1
+        for (int gi = 0; gi < NSG; gi++)
+            if (__any(gneeds(gi))) gmask |= 1u << gi;
         if (gmask == 0) continue;
         __builtin_amdgcn_wave_barrier();
         cand[lane] = mine;
@@ -501,12 +609,11 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
 #pragma unroll 1
         for (int gi = 0; gi < NSG; gi++) {
             if (!((gmask >> gi) & 1u)) continue;
-            const int64_t sg = idx * NSG + gi;  // re-test: the bound may have tightened
-            const bool need = gneed[gi] && needs_box(bvh.slo + sg * D, bvh.shi + sg * D, bvh.stag[sg]);
+            const bool need = gneeds(gi);  // re-test in registers: the bound may have tightened
             if (!__any(need)) continue;
             const int q0 = gi * SG;
             const int q1 = (int)min<int64_t>(SG, n - (idx * BT + q0)) + q0;
-#pragma unroll 4
+#pragma unroll CAND_UNROLL
             for (int qq = q0; qq < q1; qq++) {
                 const LRec<D> r = cand[qq];  // uniform address -> LDS broadcast
                 double s = sq_diff(mx[0], r.x[0]);
@@ -556,6 +663,59 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
             atomicAdd(&stats[4], (unsigned long long)(act_mask != 0));     // waves with any such lane
             stats[8 + t] = (unsigned long long)(clock64() - t_start);        // per-wave shader cycles
         }
+    }
+}
+
+// Work lists for the scan.  A lane searches unless its seed is exact (done) or its core
+// already exceeds the component bound the seeds published (it cannot supply the edge; comp_w
+// starts as all-ones bits, a NaN: no bound).  Searching lanes are compacted per group of
+// WGRP = 512 sorted positions (one level-1 BVH node), so a wave's points stay inside one
+// small Morton range: a wave takes up to P consecutive entries of one group.
+constexpr int WGRP = 512;
+
+template <int D>
+__global__ __launch_bounds__(WGRP) void group_compact_kernel(const Rec<D> *__restrict__ recs, int64_t n,
+                                                             const uint8_t *__restrict__ done,
+                                                             const unsigned long long *__restrict__ comp_w, int P,
+                                                             int32_t *__restrict__ work, int32_t *__restrict__ gcnt,
+                                                             int32_t *__restrict__ gwaves) {
+    __shared__ int wc[WGRP / 64];
+    const int64_t g = blockIdx.x;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int64_t p = g * WGRP + tid;
+    bool f = false;
+    if (p < n) {
+        const double cw = __longlong_as_double((long long)comp_w[recs[p].comp]);
+        f = !(done && done[p]) && !(recs[p].core > cw);
+    }
+    const unsigned long long m = __ballot(f);
+    const int rank = __popcll(m & ((1ull << lane) - 1));
+    if (lane == 0) wc[wv] = __popcll(m);
+    __syncthreads();
+    int base = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < WGRP / 64; k++) {
+        base += k < wv ? wc[k] : 0;
+        total += wc[k];
+    }
+    if (f) work[g * WGRP + base + rank] = (int32_t)p;
+    if (tid == 0) {
+        gcnt[g] = total;
+        gwaves[g] = (total + P - 1) / P;
+    }
+}
+
+// wave descriptors: (start in work) << 8 | count, at the group's exclusive wave offset
+__global__ void wave_desc_kernel(const int32_t *__restrict__ gcnt, const int32_t *__restrict__ woff, int64_t ngroups,
+                                 int P, unsigned long long *__restrict__ desc, int32_t *__restrict__ nwaves) {
+    HDB_GRID_STRIDE(g, ngroups) {
+        const int c = gcnt[g];
+        const int64_t o = woff[g];
+        for (int k = 0; k * P < c; k++) {
+            const int cnt = c - k * P < P ? c - k * P : P;
+            desc[o + k] = ((unsigned long long)(g * WGRP + k * P) << 8) | (unsigned long long)cnt;
+        }
+        if (g == ngroups - 1) *nwaves = (int32_t)(o + (c + P - 1) / P);
     }
 }
 
@@ -791,15 +951,21 @@ template <int D, int K, bool IDX>
 __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
                                                        Bvh bvh, int excl, double *__restrict__ lists,
                                                        int32_t *__restrict__ nb_pos, double *__restrict__ nb_s,
-                                                       unsigned long long *__restrict__ stats) {
+                                                       int pop_test, unsigned long long *__restrict__ stats) {
     __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
     __shared__ LRec<D> tile_s[4][BT];
+    __shared__ double boxs_s[4][BOXBUF * D];
+    __shared__ int32_t boxt_s[4][FAN];
+    __shared__ int64_t lvl_s[4][2 * (MAXLEV + 1)];
     const int w = threadIdx.x >> 6;
+    int64_t *off_s = lvl_s[w], *cnt_s = lvl_s[w] + MAXLEV + 1;
     const int64_t t = (int64_t)blockIdx.x * 4 + w;
     if (t >= ntiles) return;
     const int lane = threadIdx.x & 63;
     int32_t *stk = stack_s[w];
     LRec<D> *cand = tile_s[w];
+    double *bxs = boxs_s[w];
+    int32_t *bxt = boxt_s[w];
     const int64_t i = t * BT + lane;
     const bool valid = i < n;
     double mx[D];
@@ -823,27 +989,39 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
     const int32_t skip_self = excl ? mid : -2;
     unsigned long long nev = 0, n_leaf = 0, n_node = 0;
 
-    auto needs_box = [&](const double *lo, const double *hi) -> bool {
-        const double lb = box_lb2<D>(mx, lo, hi);  // loads first: one round trip per test
-        return valid & (lb < buf[K - 1]);
+    auto needs_vals = [&](const double (&a)[D], const double (&b)[D], int32_t) -> bool {
+        return valid & (box_lb2v<D>(mx, a, b) < buf[K - 1]);
     };
-    auto lane_needs = [&](int64_t node) -> bool { return needs_box(bvh.lo + node * D, bvh.hi + node * D); };
     auto scan_leaf = [&](int64_t tile, bool own) {
-        n_leaf++;
-        // the tile's 64 records: one coalesced vector load, staged in LDS (broadcast reads)
+        // the tile's 64 records (one coalesced vector load) and group boxes (cooperative
+        // staging), one round trip; the records are staged in LDS for broadcast reads
         const LRec<D> mine = fetch_rec<D>(recs, n, tile * BT + lane);
+        stage_boxes<D, NSG>(bvh.slo + tile * NSG * D, bvh.shi + tile * NSG * D, bvh.stag + tile * NSG, NSG, bxs, bxt,
+                            lane);
+        auto gneeds = [&](int gi) -> bool {
+            double a[D], b[D];
+            staged_box<D, NSG>(bxs, gi, a, b);
+            return needs_vals(a, b, 0);
+        };
+        unsigned gmask = 0;
+#pragma unroll 1
+        for (int gi = 0; gi < NSG; gi++)
+            if (own || __any(gneeds(gi))) gmask |= 1u << gi;
+        if (gmask == 0) return;
+        n_leaf++;
         __builtin_amdgcn_wave_barrier();
         cand[lane] = mine;
         __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
         for (int gi = 0; gi < NSG; gi++) {
+            if (!((gmask >> gi) & 1u)) continue;
             const int64_t sg = tile * NSG + gi;
-            if (!own && !__any(needs_box(bvh.slo + sg * D, bvh.shi + sg * D))) continue;
+            if (!own && !__any(gneeds(gi))) continue;  // re-test in registers with the current bound
             const int64_t j0 = sg * SG, j1 = min(j0 + SG, n);
             if (j1 <= j0) break;
             nev += (unsigned long long)(j1 - j0);
             const int q0 = gi * SG, q1 = q0 + (int)(j1 - j0);
-#pragma unroll 4
+#pragma unroll CAND_UNROLL
             for (int qq = q0; qq < q1; qq++) {
                 const LRec<D> r = cand[qq];  // uniform address -> LDS broadcast
                 double s = sq_diff(mx[0], r.x[0]);
@@ -856,7 +1034,13 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
         }
     };
     scan_leaf(t, true);  // own tile first: the K-th bound is tight from the start
-    const double *qlo = bvh.lo + t * D, *qhi = bvh.hi + t * D;
+    double qlo[D], qhi[D];
+#pragma unroll
+    for (int c = 0; c < D; c++) {
+        qlo[c] = bvh.lo[t * D + c];
+        qhi[c] = bvh.hi[t * D + c];
+    }
+    level_table(ntiles, off_s, cnt_s, lane);
     int sp = 0;
     if (lane == 0) stk[0] = ((bvh.levels - 1) << 26) | 0;
     sp = 1;
@@ -868,10 +1052,17 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
         const int64_t idx = code & ((1 << 26) - 1);
         n_node++;
         if (lev == 0) {
-            if (idx != t && __any(lane_needs(idx))) scan_leaf(idx, false);
+            if (idx == t) continue;
+            if (pop_test & 2) {  // re-test the popped leaf with the current K-th bound
+                stage_boxes<D, 1>(bvh.lo + idx * D, bvh.hi + idx * D, bvh.tag + idx, 1, bxs, bxt, lane);
+                double a[D], b[D];
+                staged_box<D, 1>(bxs, 0, a, b);
+                if (!__any(needs_vals(a, b, 0))) continue;
+            }
+            scan_leaf(idx, false);
             continue;
         }
-        push_children<D>(bvh, lev, idx, qlo, qhi, stk, sp, lane, lane_needs);
+        push_children<D>(bvh, off_s, cnt_s, lev, idx, qlo, qhi, stk, sp, lane, bxs, bxt, needs_vals);
     }
     if (valid) {
 #pragma unroll
@@ -1013,7 +1204,8 @@ static void knn_tree_impl(hdb_ctx *ctx, const double *X, int64_t n, bool excl, d
     {
         KernelTimer t(ctx, "knn_tree");
         hipLaunchKernelGGL((knn_tree_kernel<D, K, false>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256), 0,
-                           ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, excl ? 1 : 0, lists, nullptr, nullptr, evals);
+                           ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, excl ? 1 : 0, lists, nullptr, nullptr,
+                           ctx->trav_pop_test, evals);
         HIP_CHECK(hipGetLastError());
     }
     if (evals) {
@@ -1058,7 +1250,8 @@ static size_t boruvka_extra_bytes(int64_t n) {
     const size_t per = (size_t)n;
     auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
     return 5 * rnd(8 * per) + 5 * rnd(4 * per) + 3 * 256 + 2 * rnd(4 * per) + rnd(8 * per) +
-           rnd(8 * (per / 64 + 9));  // + diagnostics: counters and per-wave cycles (count_evals)
+           rnd(8 * (per / 16 + 72)) +  // + diagnostics: counters and per-wave cycles (count_evals)
+           rnd(4 * per) + 3 * rnd(4 * (per / WGRP + 1)) + rnd(8 * (per / 16 + 64)) + 256;  // + work lists
 }
 
 // k-NN lists over the index's sorted positions (K1t with IDX): seed every Boruvka round
@@ -1124,8 +1317,16 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
     unsigned long long *n_edges = ex.take<unsigned long long>(1);
     int32_t *ea = ex.take<int32_t>(per), *eb = ex.take<int32_t>(per);
     double *ew = ex.take<double>(per);
-    unsigned long long *evals = ctx->count_evals ? ex.take<unsigned long long>(8 + sp.ntiles) : nullptr;
     std::vector<unsigned long long> wave_cyc(ctx->count_evals ? sp.ntiles : 0);
+    const int64_t ngroups = ceil_div(n, (int64_t)WGRP);
+    const int P = ctx->boruvka_wave_pts;
+    if (P != 16 && P != 32 && P != 64) HDB_THROW(HDB_EINVAL, "boruvka_wave_pts must be 16, 32 or 64");
+    const int64_t max_waves = ngroups * (WGRP / P);
+    int32_t *work = ex.take<int32_t>(per);
+    int32_t *gcnt = ex.take<int32_t>(ngroups), *gwaves = ex.take<int32_t>(ngroups), *woff = ex.take<int32_t>(ngroups);
+    unsigned long long *desc = ex.take<unsigned long long>(max_waves);
+    int32_t *nwaves = ex.take<int32_t>(1);
+    unsigned long long *evals = ctx->count_evals ? ex.take<unsigned long long>(8 + max_waves) : nullptr;
     int64_t tot_evals = 0;
     Rec<D> *recs = sp.recs;
     int32_t *inv = sp.inv;
@@ -1169,7 +1370,7 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
         HIP_CHECK(hipMemsetAsync(comp_w, 0xff, 8 * n, st));
         HIP_CHECK(hipMemsetAsync(comp_key, 0xff, 8 * n, st));
         HIP_CHECK(hipMemsetAsync(comp_s, 0xff, 8 * n, st));
-        if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 40, st));
+        if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 8 * (8 + max_waves), st));
         if (round > 0 && ctx->boruvka_seed)
             hipLaunchKernelGGL(seed_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, inv, best_w, best_lo, best_hi,
                                comp_w);
@@ -1179,16 +1380,28 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
         {
             KernelTimer ts(ctx, "boruvka_scan");
             KernelTimer tr(ctx, round_names[round < 8 ? round : 8]);
-            hipLaunchKernelGGL(boruvka_bvh_kernel<D>, dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, st, recs, n,
-                               ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, kl ? kl->done : nullptr, evals);
+            hipLaunchKernelGGL(group_compact_kernel<D>, dim3((unsigned)ngroups), dim3(WGRP), 0, st, recs, n,
+                               kl ? kl->done : nullptr, comp_w, P, work, gcnt, gwaves);
+            size_t tb = 0;
+            HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, gwaves, woff, (int)ngroups, st));
+            void *tmp = arena(ctx, A_SORT, tb);
+            HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, gwaves, woff, (int)ngroups, st));
+            hipLaunchKernelGGL(wave_desc_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(ngroups, 256), 4096)),
+                               dim3(256), 0, st, gcnt, woff, ngroups, P, desc, nwaves);
+            hipLaunchKernelGGL(boruvka_bvh_kernel<D>, dim3((unsigned)ceil_div(max_waves, 4)), dim3(256), 0, st, recs,
+                               n, ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, work, desc, nwaves,
+                               ctx->trav_pop_test, evals);
         }
         if (evals) {
             unsigned long long h[5];
             HIP_CHECK(hipMemcpyAsync(h, evals, 40, hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
             const std::string r = "boruvka_r" + std::to_string(round);
-            HIP_CHECK(hipMemcpyAsync(wave_cyc.data(), evals + 8, 8 * sp.ntiles, hipMemcpyDeviceToHost, st));
+            wave_cyc.resize(max_waves);
+            HIP_CHECK(hipMemcpyAsync(wave_cyc.data(), evals + 8, 8 * max_waves, hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
+            wave_cyc.erase(std::remove(wave_cyc.begin(), wave_cyc.end(), 0ull), wave_cyc.end());  // exited waves
+            if (wave_cyc.empty()) wave_cyc.push_back(0);
             std::sort(wave_cyc.begin(), wave_cyc.end());
             unsigned long long cs = 0;
             for (auto c : wave_cyc) cs += c;
@@ -1293,7 +1506,7 @@ static void exact_leaf_impl(hdb_ctx *ctx, const double *X, int64_t n, int min_pt
         KernelTimer t(ctx, "knn_tree");
         hipLaunchKernelGGL((knn_tree_kernel<D, K, true>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256), 0,
                            ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, semantics == HDB_CORE_EXCL_SELF ? 1 : 0, lists,
-                           nb_pos, nb_s, stats);
+                           nb_pos, nb_s, ctx->trav_pop_test, stats);
         HIP_CHECK(hipGetLastError());
     }
     if (stats) {
