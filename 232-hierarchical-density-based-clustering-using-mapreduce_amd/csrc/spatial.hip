@@ -471,8 +471,8 @@ __device__ __forceinline__ void publish_min(unsigned long long *arr, int32_t c, 
     if (active && v < __hip_atomic_load(&arr[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(&arr[c], v);
 }
 
-template <int D>
-__global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
+template <int D, bool STATS>
+__global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
                                                           Bvh bvh, unsigned long long *__restrict__ comp_w,
                                                           double *__restrict__ best_w, double *__restrict__ best_s,
                                                           int32_t *__restrict__ best_lo, int32_t *__restrict__ best_hi,
@@ -485,6 +485,7 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
     __shared__ double boxs_s[4][BOXBUF * D];
     __shared__ int32_t boxt_s[4][FAN];
     __shared__ int64_t lvl_s[4][2 * (MAXLEV + 1)];
+    __shared__ double q_s[4][2 * D];
     const int w = threadIdx.x >> 6;
     double *bxs = boxs_s[w];
     int32_t *bxt = boxt_s[w];
@@ -493,7 +494,7 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
     // compacted work list (group_compact_kernel): wave t takes desc[t]'s run of sorted
     // positions; the grid covers the worst case, waves past the count exit
     if (t >= *nwaves) return;
-    const long long t_start = stats ? clock64() : 0;
+    const long long t_start = STATS ? clock64() : 0;
     LRec<D> *cand = tile_s[w];
     const int lane = threadIdx.x & 63;
     int32_t *stk = stack_s[w];
@@ -550,8 +551,9 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
         const bool same = (tg >= 0) & (tg == mcomp);
         return search & !(mcore > cwv) & !same & (!(bd < INFINITY) | !(lb > bd));
     };
-    // query box = the wave's own points (orders the children nearest-first)
-    double qlo[D], qhi[D];
+    // query box = the wave's own points (orders the children nearest-first); kept in LDS
+    // (only the ranking lanes read it)
+    double *qlo = q_s[w], *qhi = q_s[w] + D;
 #pragma unroll
     for (int c = 0; c < D; c++) {
         double l = valid ? mx[c] : INFINITY, h = valid ? mx[c] : -INFINITY;
@@ -559,9 +561,12 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
             l = fmin(l, __shfl_xor(l, off));
             h = fmax(h, __shfl_xor(h, off));
         }
-        qlo[c] = l;
-        qhi[c] = h;
+        if (lane == 0) {
+            qlo[c] = l;
+            qhi[c] = h;
+        }
     }
+    __builtin_amdgcn_wave_barrier();
     level_table(ntiles, off_s, cnt_s, lane);
     int sp = 0;
     if (lane == 0) stk[0] = ((bvh.levels - 1) << 26) | 0;
@@ -593,6 +598,8 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
         const LRec<D> mine = fetch_rec<D>(recs, n, idx * BT + lane);
         stage_boxes<D, NSG>(bvh.slo + idx * NSG * D, bvh.shi + idx * NSG * D, bvh.stag + idx * NSG, NSG, bxs, bxt,
                             lane);
+        cand[lane] = mine;  // staged now: the record's registers die before the culling
+        __builtin_amdgcn_wave_barrier();
         auto gneeds = [&](int gi) -> bool {
             double a[D], bb[D];
             staged_box<D, NSG>(bxs, gi, a, bb);
@@ -603,9 +610,6 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
         for (int gi = 0; gi < NSG; gi++)
             if (__any(gneeds(gi))) gmask |= 1u << gi;
         if (gmask == 0) continue;
-        __builtin_amdgcn_wave_barrier();
-        cand[lane] = mine;
-        __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
         for (int gi = 0; gi < NSG; gi++) {
             if (!((gmask >> gi) & 1u)) continue;
@@ -620,7 +624,7 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
 #pragma unroll
                 for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
                 if (!need || r.comp == mcomp) continue;
-                nev++;  // pair evaluated for a lane that needs it
+                if (STATS) nev++;  // pair evaluated for a lane that needs it
                 if (!(s <= sb)) continue;  // also drops NaN
                 double mrd = sqrt(s);  // HDBSCANStar.java:162-168 order
                 if (mcore > mrd) mrd = mcore;
@@ -652,7 +656,7 @@ __global__ __launch_bounds__(256) void boruvka_bvh_kernel(const Rec<D> *__restri
         best_hi[i] = b.hi;
     }
     publish_min(comp_w, mcomp, dbits(b.w), valid && b.w < INFINITY);
-    if (stats) {
+    if (STATS) {
         for (int off = 32; off >= 1; off >>= 1) nev += __shfl_xor(nev, off);
         const unsigned long long act_mask = __ballot(active0);
         if (lane == 0) {
@@ -947,7 +951,7 @@ __global__ void knn_seed_kernel(const Rec<D> *__restrict__ recs, int64_t n, cons
 // A visited tile is fetched with one vector load and staged in LDS; candidates are then
 // wave-uniform broadcast reads, and each lane evaluates the exact FP64 squared distance in
 // the reference's order and feeds the register top-K network.
-template <int D, int K, bool IDX>
+template <int D, int K, bool IDX, bool STATS>
 __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
                                                        Bvh bvh, int excl, double *__restrict__ lists,
                                                        int32_t *__restrict__ nb_pos, double *__restrict__ nb_s,
@@ -957,6 +961,7 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
     __shared__ double boxs_s[4][BOXBUF * D];
     __shared__ int32_t boxt_s[4][FAN];
     __shared__ int64_t lvl_s[4][2 * (MAXLEV + 1)];
+    __shared__ double q_s[4][2 * D];
     const int w = threadIdx.x >> 6;
     int64_t *off_s = lvl_s[w], *cnt_s = lvl_s[w] + MAXLEV + 1;
     const int64_t t = (int64_t)blockIdx.x * 4 + w;
@@ -998,6 +1003,8 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
         const LRec<D> mine = fetch_rec<D>(recs, n, tile * BT + lane);
         stage_boxes<D, NSG>(bvh.slo + tile * NSG * D, bvh.shi + tile * NSG * D, bvh.stag + tile * NSG, NSG, bxs, bxt,
                             lane);
+        cand[lane] = mine;  // staged now: the record's registers die before the culling
+        __builtin_amdgcn_wave_barrier();
         auto gneeds = [&](int gi) -> bool {
             double a[D], b[D];
             staged_box<D, NSG>(bxs, gi, a, b);
@@ -1009,9 +1016,6 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
             if (own || __any(gneeds(gi))) gmask |= 1u << gi;
         if (gmask == 0) return;
         n_leaf++;
-        __builtin_amdgcn_wave_barrier();
-        cand[lane] = mine;
-        __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
         for (int gi = 0; gi < NSG; gi++) {
             if (!((gmask >> gi) & 1u)) continue;
@@ -1034,12 +1038,9 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
         }
     };
     scan_leaf(t, true);  // own tile first: the K-th bound is tight from the start
-    double qlo[D], qhi[D];
-#pragma unroll
-    for (int c = 0; c < D; c++) {
-        qlo[c] = bvh.lo[t * D + c];
-        qhi[c] = bvh.hi[t * D + c];
-    }
+    double *qlo = q_s[w], *qhi = q_s[w] + D;  // query box (the own tile's) in LDS
+    if (lane < 2 * D) q_s[w][lane] = lane < D ? bvh.lo[t * D + lane] : bvh.hi[t * D + lane - D];
+    __builtin_amdgcn_wave_barrier();
     level_table(ntiles, off_s, cnt_s, lane);
     int sp = 0;
     if (lane == 0) stk[0] = ((bvh.levels - 1) << 26) | 0;
@@ -1075,7 +1076,7 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
             }
         }
     }
-    if (stats) {
+    if (STATS) {
         const unsigned long long nvalid = (unsigned long long)__popcll(__ballot(valid));
         if (lane == 0) {
             atomicAdd(&stats[0], nev * nvalid);  // (query, candidate) pairs evaluated
@@ -1203,9 +1204,14 @@ static void knn_tree_impl(hdb_ctx *ctx, const double *X, int64_t n, bool excl, d
     if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 24, ctx->stream));
     {
         KernelTimer t(ctx, "knn_tree");
-        hipLaunchKernelGGL((knn_tree_kernel<D, K, false>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256), 0,
-                           ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, excl ? 1 : 0, lists, nullptr, nullptr,
-                           ctx->trav_pop_test, evals);
+        if (evals)
+            hipLaunchKernelGGL((knn_tree_kernel<D, K, false, true>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256),
+                               0, ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, excl ? 1 : 0, lists, nullptr, nullptr,
+                               ctx->trav_pop_test, evals);
+        else
+            hipLaunchKernelGGL((knn_tree_kernel<D, K, false, false>), dim3((unsigned)ceil_div(sp.ntiles, 4)),
+                               dim3(256), 0, ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, excl ? 1 : 0, lists, nullptr,
+                               nullptr, ctx->trav_pop_test, evals);
         HIP_CHECK(hipGetLastError());
     }
     if (evals) {
@@ -1388,9 +1394,14 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, gwaves, woff, (int)ngroups, st));
             hipLaunchKernelGGL(wave_desc_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(ngroups, 256), 4096)),
                                dim3(256), 0, st, gcnt, woff, ngroups, P, desc, nwaves);
-            hipLaunchKernelGGL(boruvka_bvh_kernel<D>, dim3((unsigned)ceil_div(max_waves, 4)), dim3(256), 0, st, recs,
-                               n, ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, work, desc, nwaves,
-                               ctx->trav_pop_test, evals);
+            if (evals)
+                hipLaunchKernelGGL((boruvka_bvh_kernel<D, true>), dim3((unsigned)ceil_div(max_waves, 4)), dim3(256), 0,
+                                   st, recs, n, ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, work, desc,
+                                   nwaves, ctx->trav_pop_test, evals);
+            else
+                hipLaunchKernelGGL((boruvka_bvh_kernel<D, false>), dim3((unsigned)ceil_div(max_waves, 4)), dim3(256), 0,
+                                   st, recs, n, ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, work, desc,
+                                   nwaves, ctx->trav_pop_test, evals);
         }
         if (evals) {
             unsigned long long h[5];
@@ -1504,9 +1515,14 @@ static void exact_leaf_impl(hdb_ctx *ctx, const double *X, int64_t n, int min_pt
     if (stats) HIP_CHECK(hipMemsetAsync(stats, 0, 24, ctx->stream));
     {
         KernelTimer t(ctx, "knn_tree");
-        hipLaunchKernelGGL((knn_tree_kernel<D, K, true>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256), 0,
-                           ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, semantics == HDB_CORE_EXCL_SELF ? 1 : 0, lists,
-                           nb_pos, nb_s, ctx->trav_pop_test, stats);
+        if (stats)
+            hipLaunchKernelGGL((knn_tree_kernel<D, K, true, true>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256), 0,
+                               ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, semantics == HDB_CORE_EXCL_SELF ? 1 : 0,
+                               lists, nb_pos, nb_s, ctx->trav_pop_test, stats);
+        else
+            hipLaunchKernelGGL((knn_tree_kernel<D, K, true, false>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256),
+                               0, ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, semantics == HDB_CORE_EXCL_SELF ? 1 : 0,
+                               lists, nb_pos, nb_s, ctx->trav_pop_test, stats);
         HIP_CHECK(hipGetLastError());
     }
     if (stats) {
