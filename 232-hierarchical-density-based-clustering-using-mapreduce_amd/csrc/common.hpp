@@ -55,6 +55,7 @@ struct hdb_ctx {
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, std::pair<double, int64_t>> acc;
     hdb::Arena arenas[8];
+    int64_t *pinned = nullptr;  // pinned_words(): async device -> host counters
     int num_cus = 256;
     bool force_fp64 = false;  // disable the FP32 screen in K1 (A/B and tests)
     bool knn_tree = true;     // K1t (box-pruned) for euclidean lists when the shape allows
@@ -74,6 +75,8 @@ namespace hdb {
 enum { A_STAGE_IN = 0, A_STAGE_OUT = 1, A_WORK0 = 2, A_WORK1 = 3, A_WORK2 = 4, A_WORK3 = 5, A_PAD = 6, A_SORT = 7 };
 
 void *arena(hdb_ctx *ctx, int slot, size_t bytes);
+constexpr int PINNED_WORDS = 512;
+int64_t *pinned_words(hdb_ctx *ctx);
 // order `to` after all work queued so far on `from` (event record + stream wait)
 void stream_fence(hdb_ctx *ctx, hipStream_t from, hipStream_t to);
 

@@ -7,6 +7,12 @@ static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
 const char *last_error() { return g_last_error.c_str(); }
 
+// small pinned host buffer for asynchronous device -> host counters (PINNED_WORDS int64)
+int64_t *pinned_words(hdb_ctx *ctx) {
+    if (!ctx->pinned) HIP_CHECK(hipHostMalloc((void **)&ctx->pinned, sizeof(int64_t) * PINNED_WORDS));
+    return ctx->pinned;
+}
+
 void *arena(hdb_ctx *ctx, int slot, size_t bytes) {
     Arena &a = ctx->arenas[slot];
     if (bytes == 0) bytes = 16;
@@ -158,6 +164,7 @@ void hdb_ctx_destroy(hdb_ctx *ctx) {
     for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
     for (auto &a : ctx->arenas)
         if (a.ptr) (void)hipFree(a.ptr);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->side) {
         (void)hipStreamSynchronize(ctx->side);

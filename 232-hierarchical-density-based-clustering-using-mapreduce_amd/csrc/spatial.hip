@@ -479,6 +479,9 @@ __global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(cons
                                                           const int32_t *__restrict__ work,
                                                           const unsigned long long *__restrict__ desc,
                                                           const int32_t *__restrict__ nwaves, int pop_test,
+                                                          const int32_t *__restrict__ inv,
+                                                          int32_t *__restrict__ best_pos,
+                                                          const unsigned long long *__restrict__ n_edges_done,
                                                           unsigned long long *__restrict__ stats) {
     __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
     __shared__ LRec<D> tile_s[4][BT];
@@ -494,6 +497,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(cons
     // compacted work list (group_compact_kernel): wave t takes desc[t]'s run of sorted
     // positions; the grid covers the worst case, waves past the count exit
     if (t >= *nwaves) return;
+    if (*n_edges_done >= (unsigned long long)(n - 1)) return;  // speculative round after the last
     const long long t_start = STATS ? clock64() : 0;
     LRec<D> *cand = tile_s[w];
     const int lane = threadIdx.x & 63;
@@ -654,6 +658,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(cons
         best_s[i] = b.s;
         best_lo[i] = b.lo;
         best_hi[i] = b.hi;
+        if (b.w < INFINITY) best_pos[i] = inv[b.lo == mid ? b.hi : b.lo];  // partner, for the next seed
     }
     publish_min(comp_w, mcomp, dbits(b.w), valid && b.w < INFINITY);
     if (STATS) {
@@ -725,24 +730,22 @@ __global__ void wave_desc_kernel(const int32_t *__restrict__ gcnt, const int32_t
 
 // component minimum: comp_w = min w (published during the scan); then min s among the
 // lanes at that weight; then min (lo, hi) among the lanes at (w, s)
-template <int D>
-__global__ void comp_s_kernel(const Rec<D> *__restrict__ recs, int64_t n, const unsigned long long *__restrict__ comp_w,
+__global__ void comp_s_kernel(const int32_t *__restrict__ pcomp, int64_t n, const unsigned long long *__restrict__ comp_w,
                               const double *__restrict__ best_w, const double *__restrict__ best_s,
                               unsigned long long *__restrict__ comp_s) {
     HDB_GRID_STRIDE(i, n) {
-        int32_t c = recs[i].comp;
+        int32_t c = pcomp[i];
         double w = best_w[i];
         if (w < INFINITY && dbits(w) == comp_w[c]) atomicMin(&comp_s[c], dbits(best_s[i]));
     }
 }
 
-template <int D>
-__global__ void comp_key_kernel(const Rec<D> *__restrict__ recs, int64_t n, const unsigned long long *__restrict__ comp_w,
+__global__ void comp_key_kernel(const int32_t *__restrict__ pcomp, int64_t n, const unsigned long long *__restrict__ comp_w,
                                 const unsigned long long *__restrict__ comp_s, const double *__restrict__ best_w,
                                 const double *__restrict__ best_s, const int32_t *__restrict__ best_lo,
                                 const int32_t *__restrict__ best_hi, unsigned long long *__restrict__ comp_key) {
     HDB_GRID_STRIDE(i, n) {
-        int32_t c = recs[i].comp;
+        int32_t c = pcomp[i];
         double w = best_w[i];
         if (w < INFINITY && dbits(w) == comp_w[c] && dbits(best_s[i]) == comp_s[c])
             atomicMin(&comp_key[c], ((unsigned long long)(uint32_t)best_lo[i] << 32) | (uint32_t)best_hi[i]);
@@ -750,47 +753,56 @@ __global__ void comp_key_kernel(const Rec<D> *__restrict__ recs, int64_t n, cons
 }
 
 // per component root c: chosen edge -> parent pointer; record edge unless mutual-larger
-template <int D>
-__global__ void hook_kernel(const Rec<D> *__restrict__ recs, int64_t n, const int32_t *__restrict__ inv,
+__global__ void hook_kernel(const int32_t *__restrict__ pcomp, int64_t n, const int32_t *__restrict__ inv,
                             const unsigned long long *__restrict__ comp_w,
                             const unsigned long long *__restrict__ comp_key, int32_t *__restrict__ parent,
                             int32_t *__restrict__ out_a, int32_t *__restrict__ out_b, double *__restrict__ out_w,
                             unsigned long long *__restrict__ n_edges) {
     HDB_GRID_STRIDE(c, n) {
-        if (recs[c].comp != (int32_t)c) continue;  // not a root
+        if (pcomp[c] != (int32_t)c) continue;  // not a root
         unsigned long long k = comp_key[c];
         if (k == ~0ull) {
             parent[c] = (int32_t)c;
             continue;
         }
         int32_t lo = (int32_t)(k >> 32), hi = (int32_t)(k & 0xffffffffu);
-        int32_t cl = recs[inv[lo]].comp, ch = recs[inv[hi]].comp;
+        int32_t cl = pcomp[inv[lo]], ch = pcomp[inv[hi]];
         int32_t other = cl == (int32_t)c ? ch : cl;
         parent[c] = other;
     }
 }
 
 template <int D>
-__global__ void hook_fix_kernel(const Rec<D> *__restrict__ recs, int64_t n, const unsigned long long *__restrict__ comp_w,
+__global__ void hook_fix_kernel(const int32_t *__restrict__ pcomp, int64_t n, const unsigned long long *__restrict__ comp_w,
                                 const unsigned long long *__restrict__ comp_key, int32_t *__restrict__ parent,
                                 int32_t *__restrict__ parent2, int32_t *__restrict__ out_a, int32_t *__restrict__ out_b,
                                 double *__restrict__ out_w, unsigned long long *__restrict__ n_edges) {
-    HDB_GRID_STRIDE(c, n) {
-        if (recs[c].comp != (int32_t)c) continue;
-        int32_t p = parent[c];
-        if (p == (int32_t)c) {
-            parent2[c] = p;
-            continue;
+    const int64_t stride = (int64_t)blockDim.x * gridDim.x;
+    const int lane = threadIdx.x & 63;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {  // wave-uniform trip count
+        const int64_t c = base + threadIdx.x;
+        bool emit = false;
+        if (c < n && pcomp[c] != (int32_t)c) parent2[c] = -1;  // not a root: resolve skips it
+        if (c < n && pcomp[c] == (int32_t)c) {
+            const int32_t p = parent[c];
+            if (p == (int32_t)c) {
+                parent2[c] = p;
+            } else {
+                const bool mutual = parent[p] == (int32_t)c;
+                parent2[c] = (mutual && (int32_t)c < p) ? (int32_t)c : p;  // smaller id of a mutual pair is the root
+                emit = !(mutual && (int32_t)c > p);
+            }
         }
-        bool mutual = parent[p] == (int32_t)c;
-        if (mutual && (int32_t)c < p) {
-            parent2[c] = (int32_t)c;  // smaller id of a mutual pair becomes the root
-        } else {
-            parent2[c] = p;
-        }
-        if (!(mutual && (int32_t)c > p)) {
-            unsigned long long slot = atomicAdd(n_edges, 1ull);
-            unsigned long long k = comp_key[c];
+        // one slot reservation per wave (the edge counter is a single hot address)
+        const unsigned long long m = __ballot(emit);
+        if (m == 0) continue;
+        const int leader = __ffsll((long long)m) - 1;
+        unsigned long long slot0 = 0;
+        if (lane == leader) slot0 = atomicAdd(n_edges, (unsigned long long)__popcll(m));
+        slot0 = __shfl(slot0, leader);
+        if (emit) {
+            const unsigned long long slot = slot0 + __popcll(m & ((1ull << lane) - 1));
+            const unsigned long long k = comp_key[c];
             out_a[slot] = (int32_t)(k >> 32);
             out_b[slot] = (int32_t)(k & 0xffffffffu);
             out_w[slot] = __longlong_as_double((long long)comp_w[c]);
@@ -798,36 +810,17 @@ __global__ void hook_fix_kernel(const Rec<D> *__restrict__ recs, int64_t n, cons
     }
 }
 
-// Seeds round r > 0 from round r-1's per-point best edges: an edge whose endpoints are
-// still in different components is a valid candidate for both, so it bounds both
-// components' minimum (published to comp_w) and stays the lane's starting best; otherwise
-// the lane starts empty.  Only valid edges enter comp_w, so the final comp_w is still the
-// true component minimum (its owner lane never prunes it) -- exactness is unchanged.
-template <int D>
-__global__ void seed_kernel(const Rec<D> *__restrict__ recs, int64_t n, const int32_t *__restrict__ inv,
-                            double *__restrict__ best_w, const int32_t *__restrict__ best_lo,
-                            const int32_t *__restrict__ best_hi, unsigned long long *__restrict__ comp_w) {
-    const int64_t stride = (int64_t)blockDim.x * gridDim.x;
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {  // wave-uniform trip count
-        const int64_t i = base + threadIdx.x;
-        bool act = false;
-        int32_t ca = 0, cb = 0;
-        double w = INFINITY;
-        if (i < n) {
-            w = best_w[i];
-            if (w < INFINITY) {
-                ca = recs[inv[best_lo[i]]].comp;
-                cb = recs[inv[best_hi[i]]].comp;
-                if (ca == cb) best_w[i] = INFINITY;
-                else act = true;
-            }
-        }
-        publish_min(comp_w, ca, dbits(w), act);
-        publish_min(comp_w, cb, dbits(w), act);
+__global__ void fill_inf_kernel(double *__restrict__ p, int64_t n) { HDB_GRID_STRIDE(i, n) p[i] = INFINITY; }
+
+// per-round reset of the component minima (one launch instead of three memsets)
+__global__ void reset_comp_kernel(unsigned long long *__restrict__ a, unsigned long long *__restrict__ b,
+                                  unsigned long long *__restrict__ c, int64_t n) {
+    HDB_GRID_STRIDE(i, n) {
+        a[i] = ~0ull;
+        b[i] = ~0ull;
+        c[i] = ~0ull;
     }
 }
-
-__global__ void fill_inf_kernel(double *__restrict__ p, int64_t n) { HDB_GRID_STRIDE(i, n) p[i] = INFINITY; }
 
 // parent pointers -> the root of each hook tree in one launch (chains only shorten while
 // other lanes write: every value read is an ancestor, so the walk always ends at the root)
@@ -845,17 +838,23 @@ __global__ void resolve_kernel(int32_t *__restrict__ parent, int64_t n) {
 }
 
 template <int D>
-__global__ void relabel_kernel(Rec<D> *__restrict__ recs, int64_t n, const int32_t *__restrict__ parent) {
-    HDB_GRID_STRIDE(i, n) recs[i].comp = parent[recs[i].comp];
+__global__ void relabel_kernel(Rec<D> *__restrict__ recs, int32_t *__restrict__ pcomp, int64_t n,
+                               const int32_t *__restrict__ parent) {
+    HDB_GRID_STRIDE(i, n) {
+        const int32_t c = parent[pcomp[i]];
+        recs[i].comp = c;
+        pcomp[i] = c;
+    }
 }
+
+__global__ void pos_iota_kernel(int32_t *__restrict__ a, int64_t n) { HDB_GRID_STRIDE(i, n) a[i] = (int32_t)i; }
 
 __global__ void mark_nonroot_kernel(int32_t *__restrict__ parent, int64_t n, const int32_t *__restrict__ is_root) {
     HDB_GRID_STRIDE(c, n) if (!is_root[c]) parent[c] = -1;
 }
 
-template <int D>
-__global__ void roots_kernel(const Rec<D> *__restrict__ recs, int64_t n, int32_t *__restrict__ is_root) {
-    HDB_GRID_STRIDE(c, n) is_root[c] = recs[c].comp == (int32_t)c;
+__global__ void roots_kernel(const int32_t *__restrict__ pcomp, int64_t n, int32_t *__restrict__ is_root) {
+    HDB_GRID_STRIDE(c, n) is_root[c] = pcomp[c] == (int32_t)c;
 }
 
 __global__ void edge_idkey_kernel(const int32_t *a, const int32_t *b, int64_t m, uint64_t *k, int32_t *io) {
@@ -883,64 +882,131 @@ __global__ void set_core_kernel(Rec<D> *__restrict__ recs, int64_t n, const doub
     HDB_GRID_STRIDE(i, n) recs[i].core = core[recs[i].id];
 }
 
-// Per-round Boruvka seed from the K nearest neighbours K1t found (sorted positions, squared
-// distances).  Every list member in another component is a valid candidate; the lane keeps
-// the smaller key of those and its incoming seed (best_*: INF, or round r-1's best edge that
-// seed_kernel kept), and publishes it to comp_w so the scan starts with a component bound.
+// Block-level min publish for block-uniform loops: lanes reduce per wave (publish_min's
+// uniform case), then, when all waves of the block target one component, a single atomic.
+// Late rounds put almost every lane of a block into one huge component; one atomic per
+// wave on that address serialises at its L2 channel.
+__device__ __forceinline__ void block_publish_min(unsigned long long *arr, int32_t c, unsigned long long v,
+                                                  bool active, int32_t *s_c, unsigned long long *s_v) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const unsigned long long act = __ballot(active);
+    const int first = act ? __ffsll((long long)act) - 1 : 0;
+    const int32_t c0 = __shfl(c, first);
+    const bool uni = __all(!active || c == c0);
+    unsigned long long m = active ? v : ~0ull;
+    if (uni) {
+        for (int off = 32; off >= 1; off >>= 1) {
+            const unsigned long long o = __shfl_xor(m, off);
+            m = o < m ? o : m;
+        }
+    }
+    if (lane == 0) {
+        s_c[wv] = act == 0 ? -2 : (uni ? c0 : -1);  // -2: nothing, -1: mixed
+        s_v[wv] = m;
+    }
+    __syncthreads();
+    int32_t cb = -2;
+    unsigned long long mb = ~0ull;
+    bool block_uni = true;
+    for (int k = 0; k < nw; k++) {
+        const int32_t ck = s_c[k];
+        if (ck == -2) continue;
+        if (ck == -1 || (cb >= 0 && ck != cb)) block_uni = false;
+        cb = ck;
+        mb = s_v[k] < mb ? s_v[k] : mb;
+    }
+    __syncthreads();
+    if (block_uni) {
+        if (threadIdx.x == 0 && cb >= 0 && mb < __hip_atomic_load(&arr[cb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMin(&arr[cb], mb);
+        return;
+    }
+    if (uni) {
+        if (lane == first && act && m < __hip_atomic_load(&arr[c0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMin(&arr[c0], m);
+        return;
+    }
+    if (active && v < __hip_atomic_load(&arr[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(&arr[c], v);
+}
+
+// Per-round Boruvka seed.  (1) prev: round r-1's per-point best edge, when its endpoints are
+// still in different components, is a valid candidate (seed_kernel's rule).  (2) K > 0: the
+// K nearest neighbours K1t found (sorted positions, squared distances): every list member
+// in another component is a valid candidate.  The lane keeps the smallest key and publishes
+// it to comp_w, so the scan starts with a component bound.  Only valid edges enter comp_w,
+// so its final value is still the true component minimum.
 // The seed is provably the lane's exact best when no point outside the list can beat it:
 // every such point has s' >= s_K (the list holds every point with s' < s_K), so its weight
 // is >= LB = max(fl(sqrt(s_K)), core_p); exact if w < LB, or w == LB and s < s_K.  Exact
 // lanes skip the traversal (done[i] = 1).
 template <int D, int K>
-__global__ void knn_seed_kernel(const Rec<D> *__restrict__ recs, int64_t n, const int32_t *__restrict__ nb_pos,
-                                const double *__restrict__ nb_s, double *__restrict__ best_w, double *__restrict__ best_s,
-                                int32_t *__restrict__ best_lo, int32_t *__restrict__ best_hi,
-                                uint8_t *__restrict__ done, unsigned long long *__restrict__ comp_w) {
+__global__ __launch_bounds__(256) void round_seed_kernel(const Rec<D> *__restrict__ recs, const int32_t *__restrict__ pcomp,
+                                                        int64_t n, int prev, const int32_t *__restrict__ nb_pos,
+                                                        const double *__restrict__ nb_s, double *__restrict__ best_w,
+                                                        double *__restrict__ best_s, int32_t *__restrict__ best_lo,
+                                                        int32_t *__restrict__ best_hi, int32_t *__restrict__ best_pos,
+                                                        uint8_t *__restrict__ done, unsigned long long *__restrict__ comp_w) {
+    __shared__ int32_t s_c[4];
+    __shared__ unsigned long long s_v[4];
     const int64_t stride = (int64_t)blockDim.x * gridDim.x;
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {  // wave-uniform trip count
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {  // block-uniform trip count
         const int64_t i = base + threadIdx.x;
-        bool act = false;
         int32_t mcomp = 0;
         Best b{INFINITY, INFINITY, INT32_MAX, INT32_MAX};
         if (i < n) {
-            const Rec<D> &me = recs[i];
-            const double mcore = me.core;
-            const int32_t mid = me.id;
-            mcomp = me.comp;
-            if (best_w[i] < INFINITY) b = Best{best_w[i], best_s[i], best_lo[i], best_hi[i]};
-            double sK = -INFINITY;
-            bool full = true;
-            for (int k = 0; k < K; k++) {
-                const int32_t j = nb_pos[i * K + k];
-                const double s = nb_s[i * K + k];
-                if (j < 0 || !(s < INFINITY)) {
-                    full = false;
-                    continue;
+            mcomp = pcomp[i];
+            int32_t bpos = -1;
+            if (prev) {
+                const double w0 = best_w[i];
+                if (w0 < INFINITY) {
+                    const int32_t bp = best_pos[i];
+                    if (pcomp[bp] != mcomp) {
+                        b = Best{w0, best_s[i], best_lo[i], best_hi[i]};
+                        bpos = bp;
+                    }
                 }
-                sK = s > sK ? s : sK;
-                if (recs[j].comp == mcomp) continue;  // also the point itself (INCL lists)
-                double mrd = sqrt(s);  // HDBSCANStar.java:162-168 order, as the scan kernel
-                if (mcore > mrd) mrd = mcore;
-                const double oc = recs[j].core;
-                if (oc > mrd) mrd = oc;
-                const int32_t oid = recs[j].id;
-                const int32_t lo = mid < oid ? mid : oid, hi = mid < oid ? oid : mid;
-                if (key_less(mrd, s, lo, hi, b)) b = Best{mrd, s, lo, hi};
             }
             bool exact = false;
-            if (full && b.w < INFINITY) {
-                double lb = sqrt(sK);
-                if (mcore > lb) lb = mcore;
-                exact = (b.w < lb) || (b.w == lb && b.s < sK);
+            if (K > 0) {
+                const Rec<D> &me = recs[i];
+                const double mcore = me.core;
+                const int32_t mid = me.id;
+                double sK = -INFINITY;
+                bool full = true;
+                for (int k = 0; k < K; k++) {
+                    const int32_t j = nb_pos[i * K + k];
+                    const double s = nb_s[i * K + k];
+                    if (j < 0 || !(s < INFINITY)) {
+                        full = false;
+                        continue;
+                    }
+                    sK = s > sK ? s : sK;
+                    if (pcomp[j] == mcomp) continue;  // also the point itself (INCL lists)
+                    double mrd = sqrt(s);             // HDBSCANStar.java:162-168 order, as the scan kernel
+                    if (mcore > mrd) mrd = mcore;
+                    const double oc = recs[j].core;
+                    if (oc > mrd) mrd = oc;
+                    const int32_t oid = recs[j].id;
+                    const int32_t lo = mid < oid ? mid : oid, hi = mid < oid ? oid : mid;
+                    if (key_less(mrd, s, lo, hi, b)) {
+                        b = Best{mrd, s, lo, hi};
+                        bpos = j;
+                    }
+                }
+                if (full && b.w < INFINITY) {
+                    double lb = sqrt(sK);
+                    if (mcore > lb) lb = mcore;
+                    exact = (b.w < lb) || (b.w == lb && b.s < sK);
+                }
+                done[i] = exact ? 1 : 0;
             }
             best_w[i] = b.w;
             best_s[i] = b.s;
             best_lo[i] = b.lo;
             best_hi[i] = b.hi;
-            done[i] = exact ? 1 : 0;
-            act = b.w < INFINITY;
+            best_pos[i] = bpos;
         }
-        publish_min(comp_w, mcomp, dbits(b.w), act);
+        block_publish_min(comp_w, mcomp, dbits(b.w), i < n && b.w < INFINITY, s_c, s_v);
     }
 }
 
@@ -1257,7 +1323,8 @@ static size_t boruvka_extra_bytes(int64_t n) {
     auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
     return 5 * rnd(8 * per) + 5 * rnd(4 * per) + 3 * 256 + 2 * rnd(4 * per) + rnd(8 * per) +
            rnd(8 * (per / 16 + 72)) +  // + diagnostics: counters and per-wave cycles (count_evals)
-           rnd(4 * per) + 3 * rnd(4 * (per / WGRP + 1)) + rnd(8 * (per / 16 + 64)) + 256;  // + work lists
+           rnd(4 * per) + 3 * rnd(4 * (per / WGRP + 1)) + rnd(8 * (per / 16 + 64)) + 256 +  // + work lists
+           2 * rnd(4 * per);  // + best_pos, pcomp
 }
 
 // k-NN lists over the index's sorted positions (K1t with IDX): seed every Boruvka round
@@ -1279,6 +1346,8 @@ struct BoruvkaState {
     unsigned long long *comp_w, *comp_key, *comp_s;
     double *best_w, *best_s;
     int32_t *best_lo, *best_hi;
+    int32_t *best_pos;  // sorted position of the best edge's partner
+    int32_t *pcomp;     // component per sorted position (a compact copy of Rec::comp)
 };
 template <int D>
 static BoruvkaState<D> boruvka_state(char *extra, int64_t n, size_t *used = nullptr) {
@@ -1293,6 +1362,8 @@ static BoruvkaState<D> boruvka_state(char *extra, int64_t n, size_t *used = null
     b.comp_w = ex.take<unsigned long long>(per);
     b.comp_key = ex.take<unsigned long long>(per);
     b.comp_s = ex.take<unsigned long long>(per);
+    b.best_pos = ex.take<int32_t>(per);
+    b.pcomp = ex.take<int32_t>(per);
     if (used) *used = ex.off;
     return b;
 }
@@ -1344,45 +1415,60 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
     HIP_CHECK(hipMemsetAsync(n_edges, 0, 8, st));
     hipLaunchKernelGGL(fill_inf_kernel, dim3(g), dim3(256), 0, st, best_w, n);
     HIP_CHECK(hipGetLastError());
-    auto knn_seed = [&]() {
-        if (!kl) return;
-        const int gs = (int)std::min<int64_t>(ceil_div(n, 256), 2048);
-#define KNN_SEED(KK)                                                                                                   \
-    case KK:                                                                                                           \
-        hipLaunchKernelGGL((knn_seed_kernel<D, KK>), dim3(gs), dim3(256), 0, st, recs, n, kl->pos, kl->s, best_w,     \
-                           best_s, best_lo, best_hi, kl->done, comp_w);                                                \
-        break;
-        switch (kl->K) {
-            KNN_SEED(1)
-            KNN_SEED(3)
-            KNN_SEED(7)
-            KNN_SEED(15)
-            KNN_SEED(31)
-        default: HDB_THROW(HDB_EINVAL, "knn seed: unsupported list length");
+    int32_t *best_pos = bs.best_pos, *pcomp = bs.pcomp;
+    hipLaunchKernelGGL(pos_iota_kernel, dim3(g), dim3(256), 0, st, pcomp, n);  // comp = own position
+    auto round_seed = [&](int round) {
+        const int prev = (round > 0 && ctx->boruvka_seed) ? 1 : 0;
+        const int K = kl ? kl->K : 0;
+        if (!prev && K == 0) {
+            if (round > 0) hipLaunchKernelGGL(fill_inf_kernel, dim3(g), dim3(256), 0, st, best_w, n);
+            return;
         }
-#undef KNN_SEED
+        const int gs = (int)std::min<int64_t>(ceil_div(n, 256), 2048);
+#define ROUND_SEED(KK)                                                                                                 \
+    case KK:                                                                                                           \
+        hipLaunchKernelGGL((round_seed_kernel<D, KK>), dim3(gs), dim3(256), 0, st, recs, pcomp, n, prev,              \
+                           kl ? kl->pos : nullptr, kl ? kl->s : nullptr, best_w, best_s, best_lo, best_hi, best_pos,  \
+                           kl ? kl->done : nullptr, comp_w);                                                           \
+        break;
+        switch (K) {
+            ROUND_SEED(0)
+            ROUND_SEED(1)
+            ROUND_SEED(3)
+            ROUND_SEED(7)
+            ROUND_SEED(15)
+            ROUND_SEED(31)
+        default: HDB_THROW(HDB_EINVAL, "round seed: unsupported list length");
+        }
+#undef ROUND_SEED
         HIP_CHECK(hipGetLastError());
     };
 
     static const char *round_names[] = {"boruvka_r0", "boruvka_r1", "boruvka_r2", "boruvka_r3", "boruvka_r4",
                                         "boruvka_r5", "boruvka_r6", "boruvka_r7", "boruvka_r8+"};
-    int64_t have = 0;
-    for (int round = 0; have < n - 1; round++) {
-        if (round > 64) HDB_THROW(HDB_EINVAL, "boruvka did not converge (non-finite distances?)");
+    // Rounds are enqueued one ahead of the host's view of the edge count: the count after
+    // round r is copied to pinned memory and read only after round r+1 is queued, so the
+    // device never idles on a host round trip.  A round queued after the tree completed is a
+    // no-op (its scan exits on the count; no component has an outgoing edge to hook).
+    int64_t *hcnt = pinned_words(ctx);
+    const int max_rounds = 64;
+    std::vector<hipEvent_t> round_ev;
+    auto release_events = [&]() {
+        for (auto e : round_ev) (void)hipEventDestroy(e);
+        round_ev.clear();
+    };
+    for (int round = 0; n > 1; round++) {
+        if (round >= max_rounds || round >= PINNED_WORDS) {
+            release_events();
+            HDB_THROW(HDB_EINVAL, "boruvka did not converge (non-finite distances?)");
+        }
         hipLaunchKernelGGL(tile_comp_kernel<D>, dim3((unsigned)ntiles), dim3(64), 0, st, recs, n, tcomp, bvh.stag);
         for (int L = 1; L < bvh.levels; L++)
             hipLaunchKernelGGL(bvh_tag_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(bvh.cnt[L], 256), 4096)),
                                dim3(256), 0, st, bvh.tag, bvh.off[L - 1], bvh.cnt[L - 1], bvh.off[L], bvh.cnt[L]);
-        HIP_CHECK(hipMemsetAsync(comp_w, 0xff, 8 * n, st));
-        HIP_CHECK(hipMemsetAsync(comp_key, 0xff, 8 * n, st));
-        HIP_CHECK(hipMemsetAsync(comp_s, 0xff, 8 * n, st));
+        hipLaunchKernelGGL(reset_comp_kernel, dim3(g), dim3(256), 0, st, comp_w, comp_key, comp_s, n);
         if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 8 * (8 + max_waves), st));
-        if (round > 0 && ctx->boruvka_seed)
-            hipLaunchKernelGGL(seed_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, inv, best_w, best_lo, best_hi,
-                               comp_w);
-        else if (round > 0)
-            hipLaunchKernelGGL(fill_inf_kernel, dim3(g), dim3(256), 0, st, best_w, n);
-        knn_seed();
+        round_seed(round);
         {
             KernelTimer ts(ctx, "boruvka_scan");
             KernelTimer tr(ctx, round_names[round < 8 ? round : 8]);
@@ -1397,11 +1483,11 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             if (evals)
                 hipLaunchKernelGGL((boruvka_bvh_kernel<D, true>), dim3((unsigned)ceil_div(max_waves, 4)), dim3(256), 0,
                                    st, recs, n, ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, work, desc,
-                                   nwaves, ctx->trav_pop_test, evals);
+                                   nwaves, ctx->trav_pop_test, inv, best_pos, n_edges, evals);
             else
                 hipLaunchKernelGGL((boruvka_bvh_kernel<D, false>), dim3((unsigned)ceil_div(max_waves, 4)), dim3(256), 0,
                                    st, recs, n, ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, work, desc,
-                                   nwaves, ctx->trav_pop_test, evals);
+                                   nwaves, ctx->trav_pop_test, inv, best_pos, n_edges, evals);
         }
         if (evals) {
             unsigned long long h[5];
@@ -1427,25 +1513,32 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             ctx->stats[r + "_nodes"] = (int64_t)h[2];
             tot_evals += (int64_t)h[0];
         }
-        hipLaunchKernelGGL(comp_s_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, comp_w, best_w, best_s, comp_s);
-        hipLaunchKernelGGL(comp_key_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, comp_w, comp_s, best_w, best_s,
+        hipLaunchKernelGGL(comp_s_kernel, dim3(g), dim3(256), 0, st, pcomp, n, comp_w, best_w, best_s, comp_s);
+        hipLaunchKernelGGL(comp_key_kernel, dim3(g), dim3(256), 0, st, pcomp, n, comp_w, comp_s, best_w, best_s,
                            best_lo, best_hi, comp_key);
-        hipLaunchKernelGGL(roots_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, is_root);
-        hipLaunchKernelGGL(hook_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, inv, comp_w, comp_key, parent, ea, eb,
+        hipLaunchKernelGGL(hook_kernel, dim3(g), dim3(256), 0, st, pcomp, n, inv, comp_w, comp_key, parent, ea, eb,
                            ew, n_edges);
-        hipLaunchKernelGGL(hook_fix_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, comp_w, comp_key, parent, parent2,
+        hipLaunchKernelGGL(hook_fix_kernel<D>, dim3(g), dim3(256), 0, st, pcomp, n, comp_w, comp_key, parent, parent2,
                            ea, eb, ew, n_edges);
-        hipLaunchKernelGGL(mark_nonroot_kernel, dim3(g), dim3(256), 0, st, parent2, n, is_root);
         // hook trees -> roots (one launch, no host round trip)
         hipLaunchKernelGGL(resolve_kernel, dim3(g), dim3(256), 0, st, parent2, n);
-        hipLaunchKernelGGL(relabel_kernel<D>, dim3(g), dim3(256), 0, st, recs, n, parent2);
-        unsigned long long h_ne = 0;
-        HIP_CHECK(hipMemcpyAsync(&h_ne, n_edges, 8, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
+        hipLaunchKernelGGL(relabel_kernel<D>, dim3(g), dim3(256), 0, st, recs, pcomp, n, parent2);
+        HIP_CHECK(hipMemcpyAsync(hcnt + round, n_edges, 8, hipMemcpyDeviceToHost, st));
+        hipEvent_t ev;
+        HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        round_ev.push_back(ev);
+        HIP_CHECK(hipEventRecord(ev, st));
         HIP_CHECK(hipGetLastError());
-        if ((int64_t)h_ne == have) HDB_THROW(HDB_EINVAL, "boruvka made no progress (non-finite distances?)");
-        have = (int64_t)h_ne;
+        if (round == 0) continue;  // keep one round in flight
+        HIP_CHECK(hipEventSynchronize(round_ev[round - 1]));
+        const int64_t c = hcnt[round - 1];
+        if (c >= n - 1) break;  // the tree was complete: round `round` was a no-op
+        if (round >= 2 && c == hcnt[round - 2]) {
+            release_events();
+            HDB_THROW(HDB_EINVAL, "boruvka made no progress (non-finite distances?)");
+        }
     }
+    release_events();
     if (evals) {
         ctx->stats["boruvka_evals"] = tot_evals;
         ctx->stats["last_evals"] = tot_evals;

@@ -131,8 +131,10 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
+    # per-kernel device times: HIP events recorded on the launch stream inside the timed
+    # region (measured cost of the records: ~1% of a step)
     ctx.set_timing(True)
-    for k in ("knn_tree", "knn_sq", "boruvka_total", "boruvka_scan", "merge_sort"):
+    for k in ("knn_tree", "knn_sq", "boruvka_total", "boruvka_scan", "merge_sort", "exact_leaf_total"):
         ctx.kernel_time(k)
     barrier()
     t0 = time.perf_counter()
@@ -141,6 +143,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     ctx.set_timing(False)
+    tsteps = args.steps
     knn_ms, knn_n = ctx.kernel_time("knn_tree")
     bor_ms, bor_n = ctx.kernel_time("boruvka_total")
     scan_ms, scan_n = ctx.kernel_time("boruvka_scan")
@@ -164,13 +167,13 @@ def main():
     value = total_points * args.steps / dt
     evals = world * (n * n + n * (n - 1) / 2)  # kNN n^2 + MST n(n-1)/2
     # roofline of the dominant kernel (per launch, HIP events on the launch stream)
-    kern = {"knn_tree": (knn_ms, knn_n, knn_evals), "boruvka_scan": (scan_ms, scan_n, bor_evals * args.steps)}
+    kern = {"knn_tree": (knn_ms, knn_n, knn_evals * tsteps), "boruvka_scan": (scan_ms, scan_n, bor_evals * tsteps)}
     dom = max(kern, key=lambda k: kern[k][0])
     k_ms, k_n, k_ev = kern[dom]
     avg_s = k_ms / max(k_n, 1) / 1e3
     flops_per_launch = 3 * D * (k_ev / max(k_n, 1))  # executed pair evals x 3d flops
     achieved = flops_per_launch / avg_s / 1e12 if avg_s > 0 else 0.0
-    algo_flops = 3 * D * (n * n if dom == "knn_tree" else n * (n - 1) / 2) / max(k_n / args.steps, 1)
+    algo_flops = 3 * D * (n * n if dom == "knn_tree" else n * (n - 1) / 2) / max(k_n / tsteps, 1)
     traffic = None
     # HBM bytes per launch from the committed rocprofv3 PMC passes (tools/profile_bench.sh,
     # FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), keyed by kernel symbol
@@ -198,15 +201,15 @@ def main():
                    + (" on a second index" if args.split else ", kNN-seeded round 0 on the K1t index"), "merge": "stable desc sort",
                    "parallelism": f"partition-sharded x{world}"},
         "mrd_evals_per_s": evals * args.steps / dt,
-        "kernels_ms_per_step": {"knn_tree": knn_ms / args.steps, "boruvka_total": bor_ms / args.steps,
-                                "boruvka_scan": scan_ms / args.steps, "merge_sort": srt_ms / args.steps},
+        "kernels_ms_per_step": {"knn_tree": knn_ms / tsteps, "boruvka_total": bor_ms / tsteps,
+                                "boruvka_scan": scan_ms / tsteps, "merge_sort": srt_ms / tsteps},
         "executed_pair_evals_per_step": {"knn_tree": knn_evals, "boruvka_scan": bor_evals,
                                          "algorithmic": n * n + n * (n - 1) // 2},
         "roofline": {"bound": "fp64-valu", "kernel": dom, "achieved": achieved,
                      "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
                      "traffic": traffic, "work": "executed pair evals x 3d flops (pruned traversal)",
                      "flops_per_launch": flops_per_launch, "avg_launch_ms": avg_s * 1e3,
-                     "launches_per_step": k_n / args.steps,
+                     "launches_per_step": k_n / tsteps,
                      "algorithmic_equiv_tflops": algo_flops / avg_s / 1e12},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
