@@ -13,7 +13,8 @@ oracle for the parity tests):
   leaves  (FirstStep.java:104-120)  subsets <= processing_units (or forced, D9): cumulative
           core distances + Prim with self edges over the rows in ascending global id, one
           batched launch for all leaves <= LEAF_PRIM_MAX points; larger forced leaves use
-          the same cores + Boruvka (exact weights; topology differs from Prim only on ties)
+          hdb_exact_mst: the same cores + Boruvka on one index (exact weights; topology differs
+          from Prim only on ties)
   big subsets: D2 samples -> keyed nearest sample (FirstStep.java:74-85, D3) -> bulk
           CombineStep (D5 fold order) -> per subset LocalModelReduceByKey (D4) -> partition
           induction (Main.java:272-289, including the in-place relabel) -> LabelClassification
@@ -112,18 +113,17 @@ class MRHDBSCANStar:
             if k in by_key:
                 out.append(by_key[k])
                 continue
-            # large forced leaf (D9): cumulative cores + Boruvka (exact weights)
+            # large forced leaf (D9): cumulative cores + exact MST (Boruvka: exact weights) in one
+            # call sharing one spatial index (hdb_exact_mst)
             Xl = X.index_select(0, r).contiguous()
             n = r.shape[0]
-            core = torch.empty(n, dtype=torch.float64, device=X.device)
-            A.check(A.lib().hdb_core_distances(c.h, Xl.data_ptr(), n, X.shape[1], self.minPts, self.metric,
-                                               A.CORE_INCL_SELF_CUMULATIVE, core.data_ptr()), "leaf cores")
             ne = 2 * n - 1
             va = torch.empty(ne, dtype=torch.int32, device=X.device)
             vb = torch.empty_like(va)
             w = torch.empty(ne, dtype=torch.float64, device=X.device)
-            A.check(A.lib().hdb_mst_boruvka(c.h, Xl.data_ptr(), n, X.shape[1], core.data_ptr(), self.metric, 1,
-                                            va.data_ptr(), vb.data_ptr(), w.data_ptr()), "leaf boruvka")
+            A.check(A.lib().hdb_exact_mst(c.h, Xl.data_ptr(), n, X.shape[1], self.minPts, self.metric,
+                                          A.CORE_INCL_SELF_CUMULATIVE, 1, None, va.data_ptr(), vb.data_ptr(),
+                                          w.data_ptr()), "leaf exact MST")
             g = r.to(torch.int32)
             out.append((g[va.long()], g[vb.long()], w))
         return out
