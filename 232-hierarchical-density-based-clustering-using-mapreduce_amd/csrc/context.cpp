@@ -230,6 +230,14 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
         ctx->knn_tree = value != 0;
         return HDB_OK;
     }
+    if (k == "knn_mfma") {
+        ctx->knn_mfma = value != 0;
+        return HDB_OK;
+    }
+    if (k == "knn_mfma_min_n") {
+        ctx->knn_mfma_min_n = value;
+        return HDB_OK;
+    }
     if (k == "knn_tree_min_n") {
         ctx->knn_tree_min_n = value;
         return HDB_OK;

@@ -42,6 +42,8 @@ void bubble_knn_device(hdb_ctx *ctx, const double *rep, const double *eB, const 
 void sort_edges_desc_device(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne);
 void distance_rows_device(hdb_ctx *ctx, const double *a, const double *b, int64_t n, int d, int metric, double *out);
 bool knn_tree_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC, bool excl, double *lists);
+// K1m: MFMA-screened exact lists for 16 < d <= 256 (false: not applicable, use the FP64 scan)
+bool knn_mfma_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC, bool excl, double *lists);
 // self edges (v, v, core[v]) as FirstStep emits them after the tree edges (HDBSCANStar.java:190-203)
 void self_edges_device(hdb_ctx *ctx, const double *core, int64_t n, int32_t *va, int32_t *vb, double *w);
 void exact_leaf_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int min_pts, int metric, int semantics,

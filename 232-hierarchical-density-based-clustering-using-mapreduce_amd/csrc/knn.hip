@@ -211,6 +211,10 @@ void knn_lists_device(hdb_ctx *ctx, const double *X_dev, int64_t n, int d, int k
     if (metric == HDB_METRIC_EUCLIDEAN && !lists_i && ctx->knn_tree && n >= ctx->knn_tree_min_n &&
         knn_tree_device(ctx, X_dev, n, d, KC, excl, lists_v))
         return;
+    // high-dimensional euclidean: K1m (bf16-split MFMA screen + exact FP64 re-check)
+    if (metric == HDB_METRIC_EUCLIDEAN && !lists_i && ctx->knn_mfma && d > 16 && n >= ctx->knn_mfma_min_n &&
+        knn_mfma_device(ctx, X_dev, n, d, KC, excl, lists_v))
+        return;
     if (metric == HDB_METRIC_EUCLIDEAN) {
         int dp = (d + 1) & ~1;
         int df = d <= 4 ? 4 : (d <= 8 ? 8 : 16);
