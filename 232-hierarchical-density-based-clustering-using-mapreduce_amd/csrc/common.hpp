@@ -62,6 +62,7 @@ struct hdb_ctx {
     int64_t knn_tree_min_n = 8192;
     bool knn_mfma = true;           // K1m for euclidean lists with 16 < d <= 256
     int64_t knn_mfma_min_n = 2048;
+    bool knn_mfma_two_pass = true;  // K1m: upper-bound pass first (few exact re-checks)
     bool boruvka_seed = true;      // seed Boruvka rounds from the previous round's edges
     bool boruvka_knn_seed = true;  // exact leaf: k-NN lists seed every Boruvka round
     int boruvka_wave_pts = 64;     // points per scan wave (16/32/64), compacted per 512-position group

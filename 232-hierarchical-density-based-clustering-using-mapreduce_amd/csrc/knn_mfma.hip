@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "internal.hpp"
 
@@ -149,18 +150,34 @@ __device__ __forceinline__ double exact_sq(const double *__restrict__ a, const d
 }
 
 // ---------------------------------------------------------------- main
-template <int DP, int KC>
+// Two passes over the same MFMA pipeline:
+//  PASS_UB (0): per query, the KC smallest UPPER bounds (approx + bound) of the candidates'
+//               exact values; thr_out = the KC-th (a rigorous upper bound on the KC-th
+//               smallest exact value T*: KC distinct candidates are at or below it).  The
+//               screen here is only a heuristic (skipping candidates loosens the bound, it
+//               never invalidates it).
+//  PASS_EXACT (1): starting from thr_init, a pair is skipped only when approx - bound > thr
+//               (its exact value provably exceeds thr >= T*); survivors are re-checked in
+//               exact FP64 and merged.  With the pass-0 bound the survivors are ~KC + the
+//               few candidates within 2 bound of T*, instead of every running-minimum update
+//               of a single pass.
+// A cheap FP32 pre-screen (conservative margin) discards most pairs before the FP64 test.
+template <int DP, int KC, int PASS>
 __global__ __launch_bounds__(256) void knn_mfma_kernel(const double *__restrict__ X, int64_t n, int64_t n_pad, int d,
                                                        const __bf16 *__restrict__ Xh, const __bf16 *__restrict__ Xl,
                                                        const double *__restrict__ nrm2, const double *__restrict__ nrm,
                                                        const double *__restrict__ prm, int excl,
+                                                       const double *__restrict__ thr_init, double *__restrict__ thr_out,
                                                        double *__restrict__ lists, unsigned long long *__restrict__ stats) {
     constexpr int NS = DP / KS;  // MFMA k-steps
     constexpr int LDP = DP + 8;  // LDS row pitch (bf16): 16 B pad breaks the bank aliasing
+    constexpr int CH = DP / 8;   // 16-B chunks per row
+    constexpr int PF = MC * CH / 256;  // prefetched chunks per thread (per array)
     __shared__ __bf16 ch_s[MC * LDP];
     __shared__ __bf16 cl_s[MC * LDP];
     __shared__ double cn2_s[MC], cn_s[MC];
     __shared__ double qn2_s[MQ], qn_s[MQ], thr_s[MQ];
+    __shared__ float thrf_s[MQ];
     __shared__ int cnt_s[MQ];
     __shared__ double buf_s[MQ * MC];
 
@@ -169,6 +186,7 @@ __global__ __launch_bounds__(256) void knn_mfma_kernel(const double *__restrict_
     const int64_t qbase = (int64_t)blockIdx.x * MQ;
     const double sc = prm[1], sc2 = sc * sc;
     const double eps_dot = 2.0 * (3.1 * 0x1p-16 + 3.0 * DP * 0x1p-24) * 1.01;
+    const int ex = excl & 1;
 
     // resident query fragments (A operand): row 32wq + (lane & 31), k = 16s + 8 (lane >> 5) + j
     bf16x8 ah[NS], al[NS];
@@ -187,26 +205,46 @@ __global__ __launch_bounds__(256) void knn_mfma_kernel(const double *__restrict_
     if (tid < MQ) {
         qn2_s[tid] = nrm2[qbase + tid];
         qn_s[tid] = nrm[qbase + tid];
-        thr_s[tid] = INFINITY;
+        const double t0 = (PASS == 1 && thr_init) ? thr_init[qbase + tid] : INFINITY;
+        thr_s[tid] = t0;
+        thrf_s[tid] = (float)(t0 * sc2) * (1.0f + 1e-6f) + 1e-30f;  // rounded up (FP32 pre-screen)
         cnt_s[tid] = 0;
     }
     unsigned long long n_re = 0;
-
-    for (int64_t cbase = 0; cbase < n_pad; cbase += MC) {
-        __syncthreads();  // previous block's LDS reads are done
-        // stage the candidate block: MC rows x DP bf16, hi and lo (16-B chunks)
-        constexpr int CH = DP / 8;  // 16-B chunks per row
-        for (int e = tid; e < MC * CH; e += 256) {
+    // prefetch registers for the next candidate block
+    bf16x8 ph[PF], pl[PF];
+    double pc2 = 0, pcn = 0;
+    auto prefetch = [&](int64_t cb) {
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            const int e = tid + 256 * u;
             const int r = e / CH, c8 = (e % CH) * 8;
-            const int64_t g = (cbase + r) * DP + c8;
-            *(bf16x8 *)(ch_s + r * LDP + c8) = *(const bf16x8 *)(Xh + g);
-            *(bf16x8 *)(cl_s + r * LDP + c8) = *(const bf16x8 *)(Xl + g);
+            const int64_t g = (cb + r) * DP + c8;
+            ph[u] = *(const bf16x8 *)(Xh + g);
+            pl[u] = *(const bf16x8 *)(Xl + g);
         }
         if (tid < MC) {
-            cn2_s[tid] = nrm2[cbase + tid];
-            cn_s[tid] = nrm[cbase + tid];
+            pc2 = nrm2[cb + tid];
+            pcn = nrm[cb + tid];
+        }
+    };
+    prefetch(0);
+
+    for (int64_t cbase = 0; cbase < n_pad; cbase += MC) {
+        // park the prefetched block in LDS (the previous block's readers are past the barrier)
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            const int e = tid + 256 * u;
+            const int r = e / CH, c8 = (e % CH) * 8;
+            *(bf16x8 *)(ch_s + r * LDP + c8) = ph[u];
+            *(bf16x8 *)(cl_s + r * LDP + c8) = pl[u];
+        }
+        if (tid < MC) {
+            cn2_s[tid] = pc2;
+            cn_s[tid] = pcn;
         }
         __syncthreads();
+        if (cbase + MC < n_pad) prefetch(cbase + MC);  // in flight during the MFMAs + epilogue
         f32x16 acc;
 #pragma unroll
         for (int r = 0; r < 16; r++) acc[r] = 0.f;
@@ -220,37 +258,58 @@ __global__ __launch_bounds__(256) void knn_mfma_kernel(const double *__restrict_
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh, acc, 0, 0, 0);
         }
-        // screen + exact re-check; C layout: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+        // screen; C layout: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
         const int cc = 32 * wc + (lane & 31);
         const int64_t cid = cbase + cc;
         const double c2 = cn2_s[cc], cn = cn_s[cc];
+        const float c2f = (float)c2, cnf = (float)cn;
+        const float epsf = (float)eps_dot * 1.001f;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
             const int qr = 32 * wq + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            const float q2f = (float)qn2_s[qr];
+            // FP32 pre-screen: af is within 8 * 2^-24 (q2 + c2) of the FP64 approx; the
+            // 1e-6 (q2 + c2) margin also covers the rounding of the bound itself
+            const float af = (q2f + c2f) - 2.0f * acc[r];
+            const float bf = epsf * (float)qn_s[qr] * cnf + 1e-6f * (q2f + c2f);
+            if (af - bf > thrf_s[qr]) continue;
             const int64_t qid = qbase + qr;
-            if (qid >= n || cid >= n || (excl && qid == cid)) continue;
+            if (qid >= n || cid >= n || (ex && qid == cid)) continue;
             const double q2 = qn2_s[qr];
             const double approx = (q2 + c2) - 2.0 * (double)acc[r];
             const double bound = eps_dot * qn_s[qr] * cn + 4e-13 * (q2 + c2) + 1e-30;
-            if (approx - bound > thr_s[qr] * sc2) continue;
-            const double sx = exact_sq<DP>(X + qid * d, X + cid * d, d);
+            double val;
+            if (PASS == 0) {
+                val = (approx + bound) / sc2;  // rigorous upper bound of the exact value
+                if (!(val < thr_s[qr])) continue;
+            } else {
+                if (approx - bound > thr_s[qr] * sc2) continue;
+                val = (excl & 2) ? approx / sc2 : exact_sq<DP>(X + qid * d, X + cid * d, d);
+                n_re++;
+            }
             const int slot = atomicAdd(&cnt_s[qr], 1);
-            buf_s[qr * MC + slot] = sx;
-            n_re++;
+            buf_s[qr * MC + slot] = val;
         }
         __syncthreads();
         if (tid < MQ) {
             const int m = cnt_s[tid];
             for (int j = 0; j < m; j++) topk_insert<KC>(top, buf_s[tid * MC + j]);
             cnt_s[tid] = 0;
-            thr_s[tid] = top[KC - 1];
+            const double t = top[KC - 1] < thr_s[tid] ? top[KC - 1] : thr_s[tid];
+            thr_s[tid] = t;
+            thrf_s[tid] = (float)(t * sc2) * (1.0f + 1e-6f) + 1e-30f;
         }
+        __syncthreads();
     }
     if (tid < MQ && qbase + tid < n) {
+        if (PASS == 0) {
+            thr_out[qbase + tid] = top[KC - 1];
+        } else {
 #pragma unroll
-        for (int k = 0; k < KC; k++) {
-            const double v = top[k];
-            lists[(qbase + tid) * KC + k] = (v < INFINITY) ? sqrt(v) : JMAX;  // Java keeps Double.MAX_VALUE
+            for (int k = 0; k < KC; k++) {
+                const double v = top[k];
+                lists[(qbase + tid) * KC + k] = (v < INFINITY) ? sqrt(v) : JMAX;  // Java keeps Double.MAX_VALUE
+            }
         }
     }
     if (stats) {
@@ -265,7 +324,7 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
     const int64_t n_pad = ceil_div(n, (int64_t)MQ) * MQ;
     const int nb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, n / 64));
     auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t bytes = 2 * rnd(sizeof(__bf16) * (size_t)(n_pad * DP)) + 2 * rnd(8 * (size_t)n_pad) +
+    const size_t bytes = 2 * rnd(sizeof(__bf16) * (size_t)(n_pad * DP)) + 3 * rnd(8 * (size_t)n_pad) +
                          2 * rnd(8 * (size_t)nb * d) + rnd(8 * (size_t)d) + 256 + 256;
     char *base = (char *)arena(ctx, A_WORK3, bytes);
     size_t off = 0;
@@ -279,6 +338,8 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
     double *nrm2 = (double *)take(8 * (size_t)n_pad), *nrm = (double *)take(8 * (size_t)n_pad);
     double *psum = (double *)take(8 * (size_t)nb * d), *pmax = (double *)take(8 * (size_t)nb * d);
     double *mu = (double *)take(8 * (size_t)d);
+    double *thr = (double *)take(8 * (size_t)n_pad);
+    const bool two_pass = ctx->knn_mfma_two_pass;
     double *prm = (double *)take(256);
     unsigned long long *stats = (unsigned long long *)take(256);
     hipStream_t st = ctx->stream;
@@ -297,10 +358,15 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
     {
         KernelTimer t(ctx, "knn_mfma");
         const dim3 grid((unsigned)(n_pad / MQ));
-#define K1M_CASE(KK)                                                                                            \
-    case KK:                                                                                                    \
-        hipLaunchKernelGGL((knn_mfma_kernel<DP, KK>), grid, dim3(256), 0, st, X, n, n_pad, d, Xh, Xl, nrm2, nrm, \
-                           prm, excl ? 1 : 0, lists, ctx->count_evals ? stats : nullptr);                       \
+        const int fl = (excl ? 1 : 0) | (getenv("HDBMI_K1M_DBG") ? 2 : 0);
+#define K1M_CASE(KK)                                                                                             \
+    case KK:                                                                                                     \
+        if (two_pass)                                                                                            \
+            hipLaunchKernelGGL((knn_mfma_kernel<DP, KK, 0>), grid, dim3(256), 0, st, X, n, n_pad, d, Xh, Xl, nrm2, \
+                               nrm, prm, fl, nullptr, thr, lists, nullptr);                                     \
+        hipLaunchKernelGGL((knn_mfma_kernel<DP, KK, 1>), grid, dim3(256), 0, st, X, n, n_pad, d, Xh, Xl, nrm2,     \
+                           nrm, prm, fl, two_pass ? thr : nullptr, nullptr, lists,                               \
+                           ctx->count_evals ? stats : nullptr);                                                  \
         break;
         switch (KC) {
             K1M_CASE(1)
