@@ -21,10 +21,10 @@
 // skipped only when approx - bound > T, T = the query's current KC-th smallest exact value:
 // its exact value is then > T and could not enter the list.
 //
-// Work decomposition: a workgroup owns 64 queries (their bf16 fragments stay in VGPRs) and
-// streams all candidates in blocks of 64 through LDS; its 4 waves each produce one 32 x 32
-// tile of the 64 x 64 block.  Pairs that pass the screen are re-checked by the lane holding
-// them and appended to the query's LDS buffer; after the block, 64 owner threads merge the
+// Work decomposition: a workgroup owns 128 queries (their bf16 fragments stay in VGPRs) and
+// streams all candidates in blocks of 64 through LDS; its 8 waves each produce one 32 x 32
+// tile of the 128 x 64 block.  Pairs that pass the screen are re-checked by the lane holding
+// them and appended to the query's LDS buffer; after the block, 128 owner threads merge the
 // buffers into register top-KC lists (the same insertion network as K1) and publish the new
 // thresholds.
 #include <hip/hip_runtime.h>
@@ -40,7 +40,8 @@ namespace hdb {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int MQ = 64;  // queries per workgroup
+constexpr int MQ = 128;  // queries per workgroup (8 waves: 4 query rows x 2 candidate columns of 32)
+constexpr int NT = 512;  // threads per workgroup
 constexpr int MC = 64;  // candidates per streamed block
 constexpr int KS = 16;  // k per MFMA step
 
@@ -128,11 +129,11 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const double *__restric
 }
 
 // Exact squared distance in the reference's order (EuclideanDistance.java:28-36): the
-// additions stay sequential; the loads are issued 16 at a time (independent addresses)
-// so a re-check costs d/16 memory round trips instead of d.
+// additions stay sequential; the loads are issued 8 at a time (independent addresses)
+// so a re-check costs d/8 memory round trips instead of d.
 template <int DP>
 __device__ __forceinline__ double exact_sq(const double *__restrict__ a, const double *__restrict__ b, int d) {
-    constexpr int U = 16;
+    constexpr int U = 8;
     double sx = 0.0;  // 0 + t0^2 == t0^2 exactly (t^2 >= 0)
     for (int j0 = 0; j0 < d; j0 += U) {
         double av[U], bv[U];
@@ -163,7 +164,7 @@ __device__ __forceinline__ double exact_sq(const double *__restrict__ a, const d
 //               of a single pass.
 // A cheap FP32 pre-screen (conservative margin) discards most pairs before the FP64 test.
 template <int DP, int KC, int PASS>
-__global__ __launch_bounds__(256) void knn_mfma_kernel(const double *__restrict__ X, int64_t n, int64_t n_pad, int d,
+__global__ __launch_bounds__(NT) void knn_mfma_kernel(const double *__restrict__ X, int64_t n, int64_t n_pad, int d,
                                                        const __bf16 *__restrict__ Xh, const __bf16 *__restrict__ Xl,
                                                        const double *__restrict__ nrm2, const double *__restrict__ nrm,
                                                        const double *__restrict__ prm, int excl,
@@ -172,7 +173,7 @@ __global__ __launch_bounds__(256) void knn_mfma_kernel(const double *__restrict_
     constexpr int NS = DP / KS;  // MFMA k-steps
     constexpr int LDP = DP + 8;  // LDS row pitch (bf16): 16 B pad breaks the bank aliasing
     constexpr int CH = DP / 8;   // 16-B chunks per row
-    constexpr int PF = MC * CH / 256;  // prefetched chunks per thread (per array)
+    constexpr int PF = (MC * CH + NT - 1) / NT;  // prefetched chunks per thread (per array)
     __shared__ __bf16 ch_s[MC * LDP];
     __shared__ __bf16 cl_s[MC * LDP];
     __shared__ double cn2_s[MC], cn_s[MC];
@@ -182,7 +183,7 @@ __global__ __launch_bounds__(256) void knn_mfma_kernel(const double *__restrict_
     __shared__ double buf_s[MQ * MC];
 
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int wq = wave & 1, wc = wave >> 1;
+    const int wq = wave & 3, wc = wave >> 2;
     const int64_t qbase = (int64_t)blockIdx.x * MQ;
     const double sc = prm[1], sc2 = sc * sc;
     const double eps_dot = 2.0 * (3.1 * 0x1p-16 + 3.0 * DP * 0x1p-24) * 1.01;
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(256) void knn_mfma_kernel(const double *__restrict_
     auto prefetch = [&](int64_t cb) {
 #pragma unroll
         for (int u = 0; u < PF; u++) {
-            const int e = tid + 256 * u;
+            const int e = tid + NT * u < MC * CH ? tid + NT * u : MC * CH - 1;  // clamped (DP = 32)
             const int r = e / CH, c8 = (e % CH) * 8;
             const int64_t g = (cb + r) * DP + c8;
             ph[u] = *(const bf16x8 *)(Xh + g);
@@ -234,7 +235,8 @@ __global__ __launch_bounds__(256) void knn_mfma_kernel(const double *__restrict_
         // park the prefetched block in LDS (the previous block's readers are past the barrier)
 #pragma unroll
         for (int u = 0; u < PF; u++) {
-            const int e = tid + 256 * u;
+            const int e = tid + NT * u;
+            if (e >= MC * CH) break;
             const int r = e / CH, c8 = (e % CH) * 8;
             *(bf16x8 *)(ch_s + r * LDP + c8) = ph[u];
             *(bf16x8 *)(cl_s + r * LDP + c8) = pl[u];
@@ -362,9 +364,9 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
 #define K1M_CASE(KK)                                                                                             \
     case KK:                                                                                                     \
         if (two_pass)                                                                                            \
-            hipLaunchKernelGGL((knn_mfma_kernel<DP, KK, 0>), grid, dim3(256), 0, st, X, n, n_pad, d, Xh, Xl, nrm2, \
+            hipLaunchKernelGGL((knn_mfma_kernel<DP, KK, 0>), grid, dim3(NT), 0, st, X, n, n_pad, d, Xh, Xl, nrm2, \
                                nrm, prm, fl, nullptr, thr, lists, nullptr);                                     \
-        hipLaunchKernelGGL((knn_mfma_kernel<DP, KK, 1>), grid, dim3(256), 0, st, X, n, n_pad, d, Xh, Xl, nrm2,     \
+        hipLaunchKernelGGL((knn_mfma_kernel<DP, KK, 1>), grid, dim3(NT), 0, st, X, n, n_pad, d, Xh, Xl, nrm2,     \
                            nrm, prm, fl, two_pass ? thr : nullptr, nullptr, lists,                               \
                            ctx->count_evals ? stats : nullptr);                                                  \
         break;

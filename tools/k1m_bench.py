@@ -42,7 +42,8 @@ re_sub = ctx.get_stat("knn_mfma_rechecks")
 ctx.set_option("count_evals", 0)
 n_pad = -(-n // 64) * 64
 DP = 32 if d <= 32 else 64 if d <= 64 else 128 if d <= 128 else 256
-flops = 3 * 2.0 * n_pad * n_pad * DP
+passes = 2  # upper-bound pass + exact pass (knn_mfma_two_pass)
+flops = passes * 3 * 2.0 * n_pad * n_pad * DP  # bf16 split: 3 MFMA products per pass
 # exact spot check (Java order): 16 sampled rows
 rows = torch.randint(0, n, (16,), device="cuda", generator=g)
 bad = 0
