@@ -219,25 +219,6 @@ __global__ void tile_box_kernel(const Rec<D> *__restrict__ recs, int64_t n, doub
     }
 }
 
-template <int D>
-__global__ void tile_comp_kernel(const Rec<D> *__restrict__ recs, int64_t n, int32_t *__restrict__ tcomp,
-                                 int32_t *__restrict__ scomp) {
-    const int64_t t = blockIdx.x;
-    const int lane = threadIdx.x;
-    const int64_t i = t * BT + lane;
-    int32_t c = i < n ? recs[i].comp : -2;
-    int32_t c0 = __shfl(c, 0);
-    bool all = __all((c == c0) || (c == -2));
-    if (lane == 0) tcomp[t] = all ? c0 : -1;
-    // sub-group tags: lane g*SG holds the group's first component
-    int32_t g0 = __shfl(c, lane & ~(SG - 1));
-    unsigned long long bad = __ballot(!((c == g0) || (c == -2)));
-    if ((lane & (SG - 1)) == 0) {
-        const bool uni = ((bad >> (lane & ~(SG - 1))) & ((1ull << SG) - 1)) == 0;
-        scomp[t * NSG + lane / SG] = uni ? g0 : -1;
-    }
-}
-
 // --------------------------------------------------------------- scan
 // Edge order for K2b: (w, s, lo, hi) -- mutual-reachability weight, then the squared
 // Euclidean distance s (bitwise symmetric: (a-b)^2 == (b-a)^2 in the same dimension
@@ -289,17 +270,6 @@ __global__ void bvh_box_kernel(double *__restrict__ lo, double *__restrict__ hi,
             lo[(off + i) * D + c] = l;
             hi[(off + i) * D + c] = h;
         }
-    }
-}
-
-__global__ void bvh_tag_kernel(int32_t *__restrict__ tag, int64_t child_off, int64_t child_cnt, int64_t off,
-                               int64_t cnt) {
-    HDB_GRID_STRIDE(i, cnt) {
-        int64_t c0 = i * FAN, c1 = min(c0 + FAN, child_cnt);
-        int32_t t = tag[child_off + c0];
-        for (int64_t k = c0 + 1; k < c1 && t >= 0; k++)
-            if (tag[child_off + k] != t) t = -1;
-        tag[off + i] = t;
     }
 }
 
@@ -397,6 +367,74 @@ __device__ __forceinline__ void level_table(int64_t ntiles, int64_t *off_s, int6
         cnt_s[lane] = c;
     }
     __builtin_amdgcn_wave_barrier();
+}
+
+// Per-round relabel + component tags in one launch (one wave per tile): points take their
+// component's hook-tree root (parent2 after resolve_kernel), the tile and its 16-point groups
+// get uniform-component tags, and lane 0 folds the tile's tag into every BVH ancestor with
+// an atomic merge (EMPTY + x = x, x + x = x, else -1 "mixed") -- replacing one launch per
+// level.  A tile stops at the first ancestor already mixed: the tiles that made it mixed
+// carry their distinct tags to every higher ancestor themselves.
+constexpr int32_t TAG_EMPTY = (int32_t)0x80808080;  // memset-able marker, never a component id
+
+template <int D>
+__global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, int32_t *__restrict__ pcomp, int64_t n,
+                                                    int64_t ntiles, int levels, const int32_t *__restrict__ parent,
+                                                    int32_t *__restrict__ tag, int32_t *__restrict__ stag) {
+    __shared__ int64_t lvl_s[4][2 * (MAXLEV + 1)];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * 4 + w;
+    if (t >= ntiles) return;
+    int64_t *off_s = lvl_s[w], *cnt_s = lvl_s[w] + MAXLEV + 1;
+    if (lane <= MAXLEV) {  // level table (as bvh_shape)
+        int64_t c = ntiles, o = 0;
+        for (int l = 0; l < lane; l++) {
+            o += c;
+            c = (c + FAN - 1) / FAN;
+        }
+        off_s[lane] = o;
+        cnt_s[lane] = c;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int64_t i = t * BT + lane;
+    int32_t c = -2;
+    if (i < n) {
+        c = pcomp[i];
+        if (parent) {
+            c = parent[c];
+            recs[i].comp = c;
+            pcomp[i] = c;
+        }
+    }
+    const int32_t c0 = __shfl(c, 0);
+    const bool all = __all((c == c0) || (c == -2));
+    const int32_t tg = all ? c0 : -1;
+    const int32_t g0 = __shfl(c, lane & ~(SG - 1));
+    const unsigned long long bad = __ballot(!((c == g0) || (c == -2)));
+    if ((lane & (SG - 1)) == 0) {
+        const bool uni = ((bad >> (lane & ~(SG - 1))) & ((1ull << SG) - 1)) == 0;
+        stag[t * NSG + lane / SG] = uni ? g0 : -1;
+    }
+    if (lane == 0) {
+        tag[t] = tg;
+        for (int L = 1; L < levels; L++) {
+            int32_t *a = tag + off_s[L] + (t >> (3 * L));
+            int32_t old = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool stop = false;
+            while (true) {
+                if (old == -1) {
+                    stop = true;
+                    break;
+                }
+                const int32_t nv = (old == TAG_EMPTY || old == tg) ? tg : -1;
+                if (nv == old) break;
+                const int32_t prev = atomicCAS(a, old, nv);
+                if (prev == old) break;
+                old = prev;
+            }
+            if (stop) break;
+        }
+    }
 }
 
 // Pushes the children of internal node (lev, idx) that some lane needs, farthest first
@@ -814,11 +852,13 @@ __global__ void fill_inf_kernel(double *__restrict__ p, int64_t n) { HDB_GRID_ST
 
 // per-round reset of the component minima (one launch instead of three memsets)
 __global__ void reset_comp_kernel(unsigned long long *__restrict__ a, unsigned long long *__restrict__ b,
-                                  unsigned long long *__restrict__ c, int64_t n) {
+                                  unsigned long long *__restrict__ c, int64_t n, int32_t *__restrict__ node_tags,
+                                  int64_t n_nodes) {
     HDB_GRID_STRIDE(i, n) {
         a[i] = ~0ull;
         b[i] = ~0ull;
         c[i] = ~0ull;
+        if (i < n_nodes) node_tags[i] = TAG_EMPTY;
     }
 }
 
@@ -837,29 +877,12 @@ __global__ void resolve_kernel(int32_t *__restrict__ parent, int64_t n) {
     }
 }
 
-template <int D>
-__global__ void relabel_kernel(Rec<D> *__restrict__ recs, int32_t *__restrict__ pcomp, int64_t n,
-                               const int32_t *__restrict__ parent) {
-    HDB_GRID_STRIDE(i, n) {
-        const int32_t c = parent[pcomp[i]];
-        recs[i].comp = c;
-        pcomp[i] = c;
-    }
-}
-
 __global__ void pos_iota_kernel(int32_t *__restrict__ a, int64_t n) { HDB_GRID_STRIDE(i, n) a[i] = (int32_t)i; }
 
-__global__ void mark_nonroot_kernel(int32_t *__restrict__ parent, int64_t n, const int32_t *__restrict__ is_root) {
-    HDB_GRID_STRIDE(c, n) if (!is_root[c]) parent[c] = -1;
-}
-
-__global__ void roots_kernel(const int32_t *__restrict__ pcomp, int64_t n, int32_t *__restrict__ is_root) {
-    HDB_GRID_STRIDE(c, n) is_root[c] = pcomp[c] == (int32_t)c;
-}
-
-__global__ void edge_idkey_kernel(const int32_t *a, const int32_t *b, int64_t m, uint64_t *k, int32_t *io) {
+// (lo, hi) key packed into 2B bits (ids < 2^B), so the id sort runs only 2B radix bits
+__global__ void edge_idkey_kernel(const int32_t *a, const int32_t *b, int64_t m, int B, uint64_t *k, int32_t *io) {
     HDB_GRID_STRIDE(i, m) {
-        k[i] = ((uint64_t)(uint32_t)a[i] << 32) | (uint32_t)b[i];
+        k[i] = ((uint64_t)(uint32_t)a[i] << B) | (uint32_t)b[i];
         io[i] = (int32_t)i;
     }
 }
@@ -1317,7 +1340,7 @@ bool knn_tree_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC, bo
 
 // ------------------------------------------------------------------- K2b host
 // per-round Boruvka state carved after the index: comp_w, comp_key, comp_s, best_w, best_s
-// (8n each), best_lo/hi, parent, parent2, is_root (4n each), counters, edge lists
+// (8n each), best_lo/hi, parent, parent2 (4n each), counters, edge lists
 static size_t boruvka_extra_bytes(int64_t n) {
     const size_t per = (size_t)n;
     auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -1390,7 +1413,7 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
     unsigned long long *comp_w = bs.comp_w, *comp_key = bs.comp_key, *comp_s = bs.comp_s;
     double *best_w = bs.best_w, *best_s = bs.best_s;
     int32_t *best_lo = bs.best_lo, *best_hi = bs.best_hi;
-    int32_t *parent = ex.take<int32_t>(per), *parent2 = ex.take<int32_t>(per), *is_root = ex.take<int32_t>(per);
+    int32_t *parent = ex.take<int32_t>(per), *parent2 = ex.take<int32_t>(per);
     unsigned long long *n_edges = ex.take<unsigned long long>(1);
     int32_t *ea = ex.take<int32_t>(per), *eb = ex.take<int32_t>(per);
     double *ew = ex.take<double>(per);
@@ -1462,11 +1485,12 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             release_events();
             HDB_THROW(HDB_EINVAL, "boruvka did not converge (non-finite distances?)");
         }
-        hipLaunchKernelGGL(tile_comp_kernel<D>, dim3((unsigned)ntiles), dim3(64), 0, st, recs, n, tcomp, bvh.stag);
-        for (int L = 1; L < bvh.levels; L++)
-            hipLaunchKernelGGL(bvh_tag_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(bvh.cnt[L], 256), 4096)),
-                               dim3(256), 0, st, bvh.tag, bvh.off[L - 1], bvh.cnt[L - 1], bvh.off[L], bvh.cnt[L]);
-        hipLaunchKernelGGL(reset_comp_kernel, dim3(g), dim3(256), 0, st, comp_w, comp_key, comp_s, n);
+        // internal node tags -> EMPTY, then relabel (previous round's hook roots) + tags
+        const int64_t n_inner = bvh.off[bvh.levels] - bvh.off[1];
+        hipLaunchKernelGGL(reset_comp_kernel, dim3(g), dim3(256), 0, st, comp_w, comp_key, comp_s, n,
+                           tcomp + bvh.off[1], n_inner);
+        hipLaunchKernelGGL(retag_kernel<D>, dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, st, recs, pcomp, n,
+                           ntiles, bvh.levels, round > 0 ? parent2 : nullptr, tcomp, bvh.stag);
         if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 8 * (8 + max_waves), st));
         round_seed(round);
         {
@@ -1522,7 +1546,6 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
                            ea, eb, ew, n_edges);
         // hook trees -> roots (one launch, no host round trip)
         hipLaunchKernelGGL(resolve_kernel, dim3(g), dim3(256), 0, st, parent2, n);
-        hipLaunchKernelGGL(relabel_kernel<D>, dim3(g), dim3(256), 0, st, recs, pcomp, n, parent2);
         HIP_CHECK(hipMemcpyAsync(hcnt + round, n_edges, 8, hipMemcpyDeviceToHost, st));
         hipEvent_t ev;
         HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -1549,16 +1572,18 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
         if (ne > 0) {
             uint64_t *k1 = sp.keys, *k2 = sp.keys2;
             int32_t *p1 = sp.iota, *p2 = sp.perm;
-            hipLaunchKernelGGL(edge_idkey_kernel, dim3(g), dim3(256), 0, st, ea, eb, ne, k1, p1);
+            int B = 1;
+            while (B < 31 && ((int64_t)1 << B) < n) B++;
+            hipLaunchKernelGGL(edge_idkey_kernel, dim3(g), dim3(256), 0, st, ea, eb, ne, B, k1, p1);
             size_t tb = 0;
-            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1, k2, p1, p2, (int)ne, 0, 64, st));
+            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1, k2, p1, p2, (int)ne, 0, 2 * B, st));
             void *tmp = arena(ctx, A_SORT, tb);
-            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k1, k2, p1, p2, (int)ne, 0, 64, st));
+            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k1, k2, p1, p2, (int)ne, 0, 2 * B, st));
             hipLaunchKernelGGL(edge_wkey_kernel, dim3(g), dim3(256), 0, st, p2, ew, ne, k1);
-            // stable sort by w (non-negative doubles: bit order == numeric order)
-            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1, k2, p2, p1, (int)ne, 0, 64, st));
+            // stable sort by w (non-negative doubles: bit order == numeric order, sign bit 0)
+            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1, k2, p2, p1, (int)ne, 0, 63, st));
             tmp = arena(ctx, A_SORT, tb);
-            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k1, k2, p2, p1, (int)ne, 0, 64, st));
+            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k1, k2, p2, p1, (int)ne, 0, 63, st));
             hipLaunchKernelGGL(edge_out_kernel, dim3(g), dim3(256), 0, st, p1, ea, eb, ew, ne, va, vb, w);
             HIP_CHECK(hipGetLastError());
         }
