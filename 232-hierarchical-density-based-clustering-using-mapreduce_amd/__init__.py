@@ -8,10 +8,12 @@ from . import _capi
 from ._capi import (BUBBLE_CF, BUBBLE_COMBINESTEP, CORE_EXCL_SELF, CORE_INCL_SELF,
                     CORE_INCL_SELF_CUMULATIVE, JMAX, ArithmeticException,
                     ArrayIndexOutOfBoundsException, Context, HdbError, IllegalStateException,
-                    NullPointerException, lib)
+                    NullPointerException, NumberFormatException, lib)
 from .databubbles import (CombineStep, FirstStep, HdbscanDataBubbles, LocalModelReduceByKey,
                           bubble_stats, nearest_sample, sort_edges_desc)
 from .driver import MRHDBSCANStar
+from .formats import (MapperDataset_github, double_to_string, format_local_mst, parse_local_mst,
+                      read_dataset)
 from .hdbscanstar import (CosineSimilarity, DistanceCalculator, EuclideanDistance, HDBSCANStar,
                           ManhattanDistance, PearsonCorrelation, SupremumDistance, UndirectedGraph,
                           distance_rows, flat_labels)

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("HDBMI_LIB") or os.path.join(HERE, "lib", "libhdbmi.so
 HDB_OK = 0
 ERRORS = {
     -1: "HDB_EINVAL", -2: "HDB_EDEVICE", -3: "HDB_ENOMEM", -10: "HDB_EREF_NPE", -11: "HDB_EREF_OOB",
-    -12: "HDB_EREF_NEGATIVE_CLUSTER", -13: "HDB_EREF_DIVZERO",
+    -12: "HDB_EREF_NEGATIVE_CLUSTER", -13: "HDB_EREF_DIVZERO", -14: "HDB_EREF_NUMBER_FORMAT",
 }
 
 METRIC = {"euclidean": 0, "cosine": 1, "pearson": 2, "manhattan": 3, "supremum": 4}
@@ -48,8 +48,12 @@ class ArithmeticException(HdbError):
     pass
 
 
+class NumberFormatException(HdbError):
+    """Double.parseDouble / Integer.parseInt on a malformed field."""
+
+
 _EXC = {-10: NullPointerException, -11: ArrayIndexOutOfBoundsException, -12: IllegalStateException,
-        -13: ArithmeticException}
+        -13: ArithmeticException, -14: NumberFormatException}
 
 _lib = None
 _lock = threading.Lock()
@@ -100,6 +104,10 @@ def lib():
             "hdb_quicksort_edges": [ip, ip, dp, i64],
             "hdb_sort_edges_desc": [vp, ip, ip, dp, i64],
             "hdb_flat_labels": [vp, ip, ip, dp, i64, i64, i32, ip, lp],
+            "hdb_format_double": [C.c_double, C.c_char_p, i32],
+            "hdb_parse_points": [C.c_char_p, i64, i32, i32, dp, i64, lp, ip],
+            "hdb_format_mst_records": [ip, ip, dp, ip, ip, ip, i64, vp, i64, lp],
+            "hdb_parse_mst_records": [C.c_char_p, i64, ip, ip, dp, ip, ip, ip, i64, lp],
         }
         for name, args in sig.items():
             f = getattr(L, name)
@@ -118,7 +126,8 @@ EXPORTED = ["hdb_ctx_create", "hdb_ctx_destroy", "hdb_ctx_set_stream", "hdb_ctx_
             "hdb_distance_rows", "hdb_core_distances", "hdb_knn", "hdb_prim_mst", "hdb_prim_mst_batched",
             "hdb_leaf_msts", "hdb_mst_boruvka", "hdb_exact_mst", "hdb_nearest_sample", "hdb_bubble_stats",
             "hdb_bubble_core_distances", "hdb_bubble_prim_mst", "hdb_local_model", "hdb_quicksort_edges",
-            "hdb_sort_edges_desc", "hdb_flat_labels"]
+            "hdb_sort_edges_desc", "hdb_flat_labels", "hdb_format_double", "hdb_parse_points",
+            "hdb_format_mst_records", "hdb_parse_mst_records"]
 
 
 def check(rc: int, what: str):

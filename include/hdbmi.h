@@ -35,6 +35,7 @@ extern "C" {
 #define HDB_EREF_OOB (-11)              /* java.lang.ArrayIndexOutOfBoundsException          */
 #define HDB_EREF_NEGATIVE_CLUSTER (-12) /* Clusters.java:45-46 "Cluster cannot have less than 0 points." */
 #define HDB_EREF_DIVZERO (-13)          /* java.lang.ArithmeticException: / by zero          */
+#define HDB_EREF_NUMBER_FORMAT (-14)    /* java.lang.NumberFormatException                   */
 
 /* DistanceCalculator.getName() (distance/DistanceCalculator.java:20) */
 #define HDB_METRIC_EUCLIDEAN 0 /* EuclideanDistance.java:28-36  */
@@ -195,6 +196,38 @@ int hdb_sort_edges_desc(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64
  * min_cl_size >= 2.  ctx may be NULL when every pointer is host memory (pure host algorithm). */
 int hdb_flat_labels(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, const double *w, int64_t ne, int64_t n,
                     int32_t min_cl_size, int32_t *labels, int64_t *n_clusters);
+
+/* -------------------------------------------------- record formats (§8(f) #3)
+ * Host-only (no context, no device); see csrc/formats.cpp. */
+
+/* Double.toString(v) (Java layout, shortest round-trip digits) into buf (cap bytes, NUL
+ * terminated).  Returns the length (>= 0) or HDB_EINVAL when cap is too small (32 always
+ * suffices).  Used by the record writer below. */
+int hdb_format_double(double v, char *buf, int32_t cap);
+
+/* MapperDataset_github.call over a text file's bytes (MapperDataset_github.java:12-20):
+ * one point per line, fields Double.parseDouble'd, points numbered in file order.
+ * strict = 1: s.split(" ") exactly (a doubled space or an empty line -> NumberFormatException);
+ * strict = 0: deviation D1 (fields separated by runs of ' '/'\t', blank lines skipped, the
+ * first d fields kept).  d = 0 takes the first line's field count.  X = NULL: count only
+ * (*n_out points, *d_out columns); else X holds cap points of *d_out doubles.
+ * Errors: HDB_EREF_NUMBER_FORMAT (bad field), HDB_EREF_OOB (short line). */
+int hdb_parse_points(const char *text, int64_t len, int32_t d, int32_t strict, double *X, int64_t cap,
+                     int64_t *n_out, int32_t *d_out);
+
+/* CreateLocalMST's local-MST text (CreateLocalMST.java:110-123): "v1 v2 w f1 f2 node" per
+ * edge, '\n'-joined, no trailing newline, w via Double.toString; fake1/fake2/node nullable
+ * (written as 0).  out = NULL: *len_out = the byte length; else out (cap bytes) receives
+ * the text plus a NUL. */
+int hdb_format_mst_records(const int32_t *va, const int32_t *vb, const double *w, const int32_t *fake1,
+                           const int32_t *fake2, const int32_t *node, int64_t ne, char *out, int64_t cap,
+                           int64_t *len_out);
+
+/* UnionFindReducer.call's record parse (UnionFindReducer.java:22-45): split("\n"),
+ * split(" "), Integer.parseInt / Double.parseDouble of fields 0-5.  va = NULL: count only.
+ * Errors: HDB_EREF_OOB (fewer than 6 fields), HDB_EREF_NUMBER_FORMAT. */
+int hdb_parse_mst_records(const char *text, int64_t len, int32_t *va, int32_t *vb, double *w, int32_t *fake1,
+                          int32_t *fake2, int32_t *node, int64_t cap, int64_t *ne_out);
 
 #ifdef __cplusplus
 }
