@@ -373,8 +373,8 @@ __device__ __forceinline__ void level_table(int64_t ntiles, int64_t *off_s, int6
 // component's hook-tree root (parent2 after resolve_kernel), the tile and its 16-point groups
 // get uniform-component tags, and lane 0 folds the tile's tag into every BVH ancestor with
 // an atomic merge (EMPTY + x = x, x + x = x, else -1 "mixed") -- replacing one launch per
-// level.  A tile stops at the first ancestor already mixed: the tiles that made it mixed
-// carry their distinct tags to every higher ancestor themselves.
+// level.  A tile stops at the first ancestor already mixed or already holding its tag: the
+// tiles that wrote those values carry them to every higher ancestor themselves.
 constexpr int32_t TAG_EMPTY = (int32_t)0x80808080;  // memset-able marker, never a component id
 
 template <int D>
@@ -422,12 +422,13 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
             int32_t old = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             bool stop = false;
             while (true) {
-                if (old == -1) {
+                // already mixed, or already holding this tile's tag: the tile that wrote that
+                // value carries the same value to every higher ancestor itself
+                if (old == -1 || old == tg) {
                     stop = true;
                     break;
                 }
-                const int32_t nv = (old == TAG_EMPTY || old == tg) ? tg : -1;
-                if (nv == old) break;
+                const int32_t nv = old == TAG_EMPTY ? tg : -1;
                 const int32_t prev = atomicCAS(a, old, nv);
                 if (prev == old) break;
                 old = prev;
@@ -810,41 +811,67 @@ __global__ void hook_kernel(const int32_t *__restrict__ pcomp, int64_t n, const 
     }
 }
 
+// One workgroup covers HF_T * HF_E consecutive ids and reserves its edge slots with ONE
+// atomic: n_edges is a single hot address, and per-wave reservations (15.6k waves at 1M
+// points, most holding a root in every round) serialised at the L2 (~66 us per round).
+constexpr int HF_T = 1024, HF_E = 4;
+
 template <int D>
-__global__ void hook_fix_kernel(const int32_t *__restrict__ pcomp, int64_t n, const unsigned long long *__restrict__ comp_w,
-                                const unsigned long long *__restrict__ comp_key, int32_t *__restrict__ parent,
-                                int32_t *__restrict__ parent2, int32_t *__restrict__ out_a, int32_t *__restrict__ out_b,
-                                double *__restrict__ out_w, unsigned long long *__restrict__ n_edges) {
-    const int64_t stride = (int64_t)blockDim.x * gridDim.x;
-    const int lane = threadIdx.x & 63;
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {  // wave-uniform trip count
-        const int64_t c = base + threadIdx.x;
+__global__ __launch_bounds__(HF_T) void hook_fix_kernel(const int32_t *__restrict__ pcomp, int64_t n,
+                                                       const unsigned long long *__restrict__ comp_w,
+                                                       const unsigned long long *__restrict__ comp_key,
+                                                       int32_t *__restrict__ parent, int32_t *__restrict__ parent2,
+                                                       int32_t *__restrict__ out_a, int32_t *__restrict__ out_b,
+                                                       double *__restrict__ out_w, unsigned long long *__restrict__ n_edges) {
+    __shared__ int wcnt[HF_T / 64];
+    __shared__ unsigned long long sbase;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t c0 = (int64_t)blockIdx.x * (HF_T * HF_E) + threadIdx.x;
+    unsigned long long m[HF_E];
+    int wtot = 0;
+#pragma unroll
+    for (int e = 0; e < HF_E; e++) {
+        const int64_t c = c0 + (int64_t)e * HF_T;  // coalesced: consecutive lanes, consecutive ids
         bool emit = false;
-        if (c < n && pcomp[c] != (int32_t)c) parent2[c] = -1;  // not a root: resolve skips it
-        if (c < n && pcomp[c] == (int32_t)c) {
-            const int32_t p = parent[c];
-            if (p == (int32_t)c) {
-                parent2[c] = p;
+        if (c < n) {
+            if (pcomp[c] != (int32_t)c) {
+                parent2[c] = -1;  // not a root: resolve skips it
             } else {
-                const bool mutual = parent[p] == (int32_t)c;
-                parent2[c] = (mutual && (int32_t)c < p) ? (int32_t)c : p;  // smaller id of a mutual pair is the root
-                emit = !(mutual && (int32_t)c > p);
+                const int32_t p = parent[c];
+                if (p == (int32_t)c) {
+                    parent2[c] = p;
+                } else {
+                    const bool mutual = parent[p] == (int32_t)c;
+                    parent2[c] = (mutual && (int32_t)c < p) ? (int32_t)c : p;  // smaller id of a mutual pair is the root
+                    emit = !(mutual && (int32_t)c > p);
+                }
             }
         }
-        // one slot reservation per wave (the edge counter is a single hot address)
-        const unsigned long long m = __ballot(emit);
-        if (m == 0) continue;
-        const int leader = __ffsll((long long)m) - 1;
-        unsigned long long slot0 = 0;
-        if (lane == leader) slot0 = atomicAdd(n_edges, (unsigned long long)__popcll(m));
-        slot0 = __shfl(slot0, leader);
-        if (emit) {
-            const unsigned long long slot = slot0 + __popcll(m & ((1ull << lane) - 1));
+        m[e] = __ballot(emit);
+        wtot += __popcll(m[e]);
+    }
+    if (lane == 0) wcnt[wv] = wtot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int k = 0; k < HF_T / 64; k++) tot += wcnt[k];
+        sbase = tot ? atomicAdd(n_edges, (unsigned long long)tot) : 0;
+    }
+    __syncthreads();
+    unsigned long long slot = sbase;
+    for (int k = 0; k < wv; k++) slot += (unsigned long long)wcnt[k];
+    const unsigned long long below = (1ull << lane) - 1;
+#pragma unroll
+    for (int e = 0; e < HF_E; e++) {
+        if ((m[e] >> lane) & 1ull) {
+            const int64_t c = c0 + (int64_t)e * HF_T;
+            const unsigned long long sl = slot + __popcll(m[e] & below);
             const unsigned long long k = comp_key[c];
-            out_a[slot] = (int32_t)(k >> 32);
-            out_b[slot] = (int32_t)(k & 0xffffffffu);
-            out_w[slot] = __longlong_as_double((long long)comp_w[c]);
+            out_a[sl] = (int32_t)(k >> 32);
+            out_b[sl] = (int32_t)(k & 0xffffffffu);
+            out_w[sl] = __longlong_as_double((long long)comp_w[c]);
         }
+        slot += __popcll(m[e]);
     }
 }
 
@@ -1542,7 +1569,8 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
                            best_lo, best_hi, comp_key);
         hipLaunchKernelGGL(hook_kernel, dim3(g), dim3(256), 0, st, pcomp, n, inv, comp_w, comp_key, parent, ea, eb,
                            ew, n_edges);
-        hipLaunchKernelGGL(hook_fix_kernel<D>, dim3(g), dim3(256), 0, st, pcomp, n, comp_w, comp_key, parent, parent2,
+        hipLaunchKernelGGL(hook_fix_kernel<D>, dim3((unsigned)ceil_div(n, (int64_t)HF_T * HF_E)), dim3(HF_T), 0, st,
+                           pcomp, n, comp_w, comp_key, parent, parent2,
                            ea, eb, ew, n_edges);
         // hook trees -> roots (one launch, no host round trip)
         hipLaunchKernelGGL(resolve_kernel, dim3(g), dim3(256), 0, st, parent2, n);
