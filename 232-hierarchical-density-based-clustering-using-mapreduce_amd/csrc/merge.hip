@@ -7,6 +7,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "common.hpp"
+#include "sort.hpp"
 
 namespace hdb {
 
@@ -53,11 +54,9 @@ void sort_edges_desc_device(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, i
     KernelTimer t(ctx, "merge_sort");
     hipLaunchKernelGGL(edge_keys_kernel, dim3(g), dim3(256), 0, ctx->stream, w, ne, keys, iota);
     size_t tb = 0;
-    HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, keys, keys2, iota, perm, (int)ne, 0, 64,
-                                                           ctx->stream));
+    HIP_CHECK(sort_pairs_desc(nullptr, tb, keys, keys2, iota, perm, ne, 0, 64, ctx->stream));
     void *tmp = arena(ctx, A_SORT, tb);
-    HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(tmp, tb, keys, keys2, iota, perm, (int)ne, 0, 64,
-                                                           ctx->stream));
+    HIP_CHECK(sort_pairs_desc(tmp, tb, keys, keys2, iota, perm, ne, 0, 64, ctx->stream));
     hipLaunchKernelGGL(edge_gather_kernel, dim3(g), dim3(256), 0, ctx->stream, perm, ne, va, vb, w, ta, tb_, tw);
     HIP_CHECK(hipMemcpyAsync(va, ta, sizeof(int32_t) * ne, hipMemcpyDeviceToDevice, ctx->stream));
     HIP_CHECK(hipMemcpyAsync(vb, tb_, sizeof(int32_t) * ne, hipMemcpyDeviceToDevice, ctx->stream));

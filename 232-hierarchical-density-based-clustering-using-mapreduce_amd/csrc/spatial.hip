@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "internal.hpp"
+#include "sort.hpp"
 
 namespace hdb {
 
@@ -148,10 +149,19 @@ __global__ void bbox_final_kernel(const double *__restrict__ part, int nb, doubl
     }
 }
 
+// Morton bits per dimension: at most 16 (65,536 cells per axis is far below the point
+// spacing that matters for 64-point tiles) so the key sort runs 48 bits (6 onesweep passes)
+// instead of 63 (8).  The order only shapes the index; every result is order-independent.
+__host__ __device__ inline int morton_bits(int d) {
+    const int dk = d < 8 ? d : 8;
+    const int b = 63 / dk;
+    return b > 16 ? 16 : b;
+}
+
 __global__ void morton_kernel(const double *__restrict__ X, int64_t n, int d, const double *__restrict__ lo,
                               const double *__restrict__ hi, uint64_t *__restrict__ keys, int32_t *__restrict__ iota) {
     const int dk = d < 8 ? d : 8;
-    const int bits = 63 / dk > 21 ? 21 : 63 / dk;
+    const int bits = morton_bits(d);
     HDB_GRID_STRIDE(i, n) {
         uint64_t key = 0;
         uint32_t q[8];
@@ -521,6 +531,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(cons
                                                           const int32_t *__restrict__ inv,
                                                           int32_t *__restrict__ best_pos,
                                                           const unsigned long long *__restrict__ n_edges_done,
+                                                          double *__restrict__ lbw, uint8_t *__restrict__ xact,
                                                           unsigned long long *__restrict__ stats) {
     __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
     __shared__ LRec<D> tile_s[4][BT];
@@ -547,6 +558,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(cons
     unsigned long long n_leaf = 0, nev = 0;
     double mx[D];
     double mcore = 0;
+    double mlb = 0;  // lower bound of the lane's best weight: max(core, bound kept from earlier rounds)
     int32_t mcomp = -3, mid = 0;
     if (valid) {
         const Rec<D> r = recs[i];
@@ -555,6 +567,8 @@ __global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(cons
         mcore = r.core;
         mcomp = r.comp;
         mid = r.id;
+        const double l = lbw[i];
+        mlb = mcore > l ? mcore : l;
     } else {
 #pragma unroll
         for (int c = 0; c < D; c++) mx[c] = 0;
@@ -584,7 +598,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(cons
     auto bound = [&]() -> double { return sb < cb2 ? sb : cb2; };
     const bool search = valid;  // done / dead lanes are not in the work list
     refresh();  // the seeds already bound the component (seed kernels publish before the scan)
-    const bool active0 = search && !(mcore > cwv);
+    const bool active0 = search && !(mlb > cwv);
     // MRD >= own core (HDBSCANStar.java:164-166): a lane whose core exceeds the component
     // bound cannot supply the component's edge (false for a NaN core, which never raises MRD).
     // Branch-free so the box loads are not sunk into conditional blocks.
@@ -592,7 +606,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(cons
         const double lb = box_lb2v<D>(mx, a, b);
         const double bd = bound();
         const bool same = (tg >= 0) & (tg == mcomp);
-        return search & !(mcore > cwv) & !same & (!(bd < INFINITY) | !(lb > bd));
+        return search & !(mlb > cwv) & !same & (!(bd < INFINITY) | !(lb > bd));
     };
     // query box = the wave's own points (orders the children nearest-first); kept in LDS
     // (only the ranking lanes read it)
@@ -698,6 +712,14 @@ __global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(cons
         best_lo[i] = b.lo;
         best_hi[i] = b.hi;
         if (b.w < INFINITY) best_pos[i] = inv[b.lo == mid ? b.hi : b.lo];  // partner, for the next seed
+        // Bounds carried to later rounds (a component only grows, so a point's best over the
+        // shrinking outside set never decreases).  Candidates the component bound pruned have
+        // w > cwv; a lane that stopped (mlb > cwv) has best >= mlb.  So best >= min(b.w, cwv)
+        // always, and b is the exact (key-minimal) best iff the lane never stopped and
+        // b.w <= cwv.
+        const double lb = b.w < cwv ? b.w : cwv;
+        if (lb > lbw[i]) lbw[i] = lb;
+        xact[i] = (!(mlb > cwv) && b.w <= cwv) ? 1 : 0;
     }
     publish_min(comp_w, mcomp, dbits(b.w), valid && b.w < INFINITY);
     if (STATS) {
@@ -724,6 +746,7 @@ constexpr int WGRP = 512;
 template <int D>
 __global__ __launch_bounds__(WGRP) void group_compact_kernel(const Rec<D> *__restrict__ recs, int64_t n,
                                                              const uint8_t *__restrict__ done,
+                                                             const double *__restrict__ lbw,
                                                              const unsigned long long *__restrict__ comp_w, int P,
                                                              int32_t *__restrict__ work, int32_t *__restrict__ gcnt,
                                                              int32_t *__restrict__ gwaves) {
@@ -734,7 +757,8 @@ __global__ __launch_bounds__(WGRP) void group_compact_kernel(const Rec<D> *__res
     bool f = false;
     if (p < n) {
         const double cw = __longlong_as_double((long long)comp_w[recs[p].comp]);
-        f = !(done && done[p]) && !(recs[p].core > cw);
+        const double c = recs[p].core, l = lbw[p];
+        f = !(done && done[p]) && !((c > l ? c : l) > cw);
     }
     const unsigned long long m = __ballot(f);
     const int rank = __popcll(m & ((1ull << lane) - 1));
@@ -995,7 +1019,8 @@ __global__ __launch_bounds__(256) void round_seed_kernel(const Rec<D> *__restric
                                                         const double *__restrict__ nb_s, double *__restrict__ best_w,
                                                         double *__restrict__ best_s, int32_t *__restrict__ best_lo,
                                                         int32_t *__restrict__ best_hi, int32_t *__restrict__ best_pos,
-                                                        uint8_t *__restrict__ done, unsigned long long *__restrict__ comp_w) {
+                                                        uint8_t *__restrict__ done, double *__restrict__ lbw,
+                                                        uint8_t *__restrict__ xact, unsigned long long *__restrict__ comp_w) {
     __shared__ int32_t s_c[4];
     __shared__ unsigned long long s_v[4];
     const int64_t stride = (int64_t)blockDim.x * gridDim.x;
@@ -1006,6 +1031,7 @@ __global__ __launch_bounds__(256) void round_seed_kernel(const Rec<D> *__restric
         if (i < n) {
             mcomp = pcomp[i];
             int32_t bpos = -1;
+            bool exact = false;
             if (prev) {
                 const double w0 = best_w[i];
                 if (w0 < INFINITY) {
@@ -1013,10 +1039,12 @@ __global__ __launch_bounds__(256) void round_seed_kernel(const Rec<D> *__restric
                     if (pcomp[bp] != mcomp) {
                         b = Best{w0, best_s[i], best_lo[i], best_hi[i]};
                         bpos = bp;
+                        // last round's exact best is still outside the component: still exact
+                        // (the outside set only shrank), so the lane skips the traversal
+                        exact = xact[i] != 0;
                     }
                 }
             }
-            bool exact = false;
             if (K > 0) {
                 const Rec<D> &me = recs[i];
                 const double mcore = me.core;
@@ -1043,13 +1071,15 @@ __global__ __launch_bounds__(256) void round_seed_kernel(const Rec<D> *__restric
                         bpos = j;
                     }
                 }
-                if (full && b.w < INFINITY) {
+                if (!exact && full && b.w < INFINITY) {
                     double lb = sqrt(sK);
                     if (mcore > lb) lb = mcore;
                     exact = (b.w < lb) || (b.w == lb && b.s < sK);
                 }
-                done[i] = exact ? 1 : 0;
             }
+            if (done) done[i] = exact ? 1 : 0;
+            xact[i] = exact ? 1 : 0;
+            if (exact && b.w > lbw[i]) lbw[i] = b.w;
             best_w[i] = b.w;
             best_s[i] = b.s;
             best_lo[i] = b.lo;
@@ -1282,9 +1312,10 @@ static Spatial<D> build_spatial(hdb_ctx *ctx, const double *X, int64_t n, const 
     hipLaunchKernelGGL(morton_kernel, dim3(g), dim3(256), 0, st, X, n, D, blo, bhi, sp.keys, sp.iota);
     {
         size_t tb = 0;
-        HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, sp.keys, sp.keys2, sp.iota, sp.perm, (int)n, 0, 64, st));
+        const int kbits = (D < 8 ? D : 8) * morton_bits(D);
+        HIP_CHECK(sort_pairs(nullptr, tb, sp.keys, sp.keys2, sp.iota, sp.perm, n, 0, kbits, st));
         void *tmp = arena(ctx, A_SORT, tb);
-        HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, sp.keys, sp.keys2, sp.iota, sp.perm, (int)n, 0, 64, st));
+        HIP_CHECK(sort_pairs(tmp, tb, sp.keys, sp.keys2, sp.iota, sp.perm, n, 0, kbits, st));
     }
     hipLaunchKernelGGL(build_recs_kernel<D>, dim3(g), dim3(256), 0, st, X, core, sp.perm, n, sp.recs, sp.inv);
     hipLaunchKernelGGL(tile_box_kernel<D>, dim3((unsigned)sp.ntiles), dim3(64), 0, st, sp.recs, n, sp.bvh.lo,
@@ -1374,7 +1405,7 @@ static size_t boruvka_extra_bytes(int64_t n) {
     return 5 * rnd(8 * per) + 5 * rnd(4 * per) + 3 * 256 + 2 * rnd(4 * per) + rnd(8 * per) +
            rnd(8 * (per / 16 + 72)) +  // + diagnostics: counters and per-wave cycles (count_evals)
            rnd(4 * per) + 3 * rnd(4 * (per / WGRP + 1)) + rnd(8 * (per / 16 + 64)) + 256 +  // + work lists
-           2 * rnd(4 * per);  // + best_pos, pcomp
+           2 * rnd(4 * per) + rnd(8 * per) + rnd(per);  // + best_pos, pcomp, lbw, xact
 }
 
 // k-NN lists over the index's sorted positions (K1t with IDX): seed every Boruvka round
@@ -1398,6 +1429,8 @@ struct BoruvkaState {
     int32_t *best_lo, *best_hi;
     int32_t *best_pos;  // sorted position of the best edge's partner
     int32_t *pcomp;     // component per sorted position (a compact copy of Rec::comp)
+    double *lbw;        // per point: lower bound of its best outgoing weight (monotone over rounds)
+    uint8_t *xact;      // per point: best_* is the exact best of the last round
 };
 template <int D>
 static BoruvkaState<D> boruvka_state(char *extra, int64_t n, size_t *used = nullptr) {
@@ -1414,6 +1447,8 @@ static BoruvkaState<D> boruvka_state(char *extra, int64_t n, size_t *used = null
     b.comp_s = ex.take<unsigned long long>(per);
     b.best_pos = ex.take<int32_t>(per);
     b.pcomp = ex.take<int32_t>(per);
+    b.lbw = ex.take<double>(per);
+    b.xact = ex.take<uint8_t>(per);
     if (used) *used = ex.off;
     return b;
 }
@@ -1464,6 +1499,8 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
     hipStream_t st = ctx->stream;
     HIP_CHECK(hipMemsetAsync(n_edges, 0, 8, st));
     hipLaunchKernelGGL(fill_inf_kernel, dim3(g), dim3(256), 0, st, best_w, n);
+    HIP_CHECK(hipMemsetAsync(bs.lbw, 0, sizeof(double) * per, st));  // +0.0: no bound yet
+    HIP_CHECK(hipMemsetAsync(bs.xact, 0, per, st));
     HIP_CHECK(hipGetLastError());
     int32_t *best_pos = bs.best_pos, *pcomp = bs.pcomp;
     hipLaunchKernelGGL(pos_iota_kernel, dim3(g), dim3(256), 0, st, pcomp, n);  // comp = own position
@@ -1479,7 +1516,7 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
     case KK:                                                                                                           \
         hipLaunchKernelGGL((round_seed_kernel<D, KK>), dim3(gs), dim3(256), 0, st, recs, pcomp, n, prev,              \
                            kl ? kl->pos : nullptr, kl ? kl->s : nullptr, best_w, best_s, best_lo, best_hi, best_pos,  \
-                           kl ? kl->done : nullptr, comp_w);                                                           \
+                           kl ? kl->done : nullptr, bs.lbw, bs.xact, comp_w);                                          \
         break;
         switch (K) {
             ROUND_SEED(0)
@@ -1524,7 +1561,7 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             KernelTimer ts(ctx, "boruvka_scan");
             KernelTimer tr(ctx, round_names[round < 8 ? round : 8]);
             hipLaunchKernelGGL(group_compact_kernel<D>, dim3((unsigned)ngroups), dim3(WGRP), 0, st, recs, n,
-                               kl ? kl->done : nullptr, comp_w, P, work, gcnt, gwaves);
+                               kl ? kl->done : nullptr, bs.lbw, comp_w, P, work, gcnt, gwaves);
             size_t tb = 0;
             HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, gwaves, woff, (int)ngroups, st));
             void *tmp = arena(ctx, A_SORT, tb);
@@ -1534,11 +1571,11 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             if (evals)
                 hipLaunchKernelGGL((boruvka_bvh_kernel<D, true>), dim3((unsigned)ceil_div(max_waves, 4)), dim3(256), 0,
                                    st, recs, n, ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, work, desc,
-                                   nwaves, ctx->trav_pop_test, inv, best_pos, n_edges, evals);
+                                   nwaves, ctx->trav_pop_test, inv, best_pos, n_edges, bs.lbw, bs.xact, evals);
             else
                 hipLaunchKernelGGL((boruvka_bvh_kernel<D, false>), dim3((unsigned)ceil_div(max_waves, 4)), dim3(256), 0,
                                    st, recs, n, ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, work, desc,
-                                   nwaves, ctx->trav_pop_test, inv, best_pos, n_edges, evals);
+                                   nwaves, ctx->trav_pop_test, inv, best_pos, n_edges, bs.lbw, bs.xact, evals);
         }
         if (evals) {
             unsigned long long h[5];
@@ -1604,14 +1641,14 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             while (B < 31 && ((int64_t)1 << B) < n) B++;
             hipLaunchKernelGGL(edge_idkey_kernel, dim3(g), dim3(256), 0, st, ea, eb, ne, B, k1, p1);
             size_t tb = 0;
-            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1, k2, p1, p2, (int)ne, 0, 2 * B, st));
+            HIP_CHECK(sort_pairs(nullptr, tb, k1, k2, p1, p2, ne, 0, 2 * B, st));
             void *tmp = arena(ctx, A_SORT, tb);
-            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k1, k2, p1, p2, (int)ne, 0, 2 * B, st));
+            HIP_CHECK(sort_pairs(tmp, tb, k1, k2, p1, p2, ne, 0, 2 * B, st));
             hipLaunchKernelGGL(edge_wkey_kernel, dim3(g), dim3(256), 0, st, p2, ew, ne, k1);
             // stable sort by w (non-negative doubles: bit order == numeric order, sign bit 0)
-            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1, k2, p2, p1, (int)ne, 0, 63, st));
+            HIP_CHECK(sort_pairs(nullptr, tb, k1, k2, p2, p1, ne, 0, 63, st));
             tmp = arena(ctx, A_SORT, tb);
-            HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k1, k2, p2, p1, (int)ne, 0, 63, st));
+            HIP_CHECK(sort_pairs(tmp, tb, k1, k2, p2, p1, ne, 0, 63, st));
             hipLaunchKernelGGL(edge_out_kernel, dim3(g), dim3(256), 0, st, p1, ea, eb, ew, ne, va, vb, w);
             HIP_CHECK(hipGetLastError());
         }
