@@ -64,6 +64,8 @@ struct hdb_ctx {
     int64_t knn_mfma_min_n = 2048;
     bool knn_mfma_two_pass = true;  // K1m: upper-bound pass first (few exact re-checks)
     bool boruvka_seed = true;      // seed Boruvka rounds from the previous round's edges
+    int leaf_seed_k = -1;          // exact leaf: k-NN list length at least this (-1: by dimension)
+    int leaf_list_rounds = 2;      // exact leaf: Boruvka rounds seeded from the k-NN lists (A/B: tools/seedk_ab.py)
     bool boruvka_knn_seed = true;  // exact leaf: k-NN lists seed every Boruvka round
     int boruvka_wave_pts = 64;     // points per scan wave (16/32/64), compacted per 512-position group
     int trav_pop_test = 0;         // bit 0: Boruvka re-tests a popped node, bit 1: K1t a popped leaf

@@ -250,6 +250,16 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
         ctx->prim_coop = value != 0;
         return HDB_OK;
     }
+    if (k == "leaf_seed_k") {
+        if (value < -1 || value > 31) return HDB_EINVAL;
+        ctx->leaf_seed_k = (int)value;
+        return HDB_OK;
+    }
+    if (k == "leaf_list_rounds") {
+        if (value < 0) return HDB_EINVAL;
+        ctx->leaf_list_rounds = (int)value;
+        return HDB_OK;
+    }
     if (k == "boruvka_seed") {
         ctx->boruvka_seed = value != 0;
         return HDB_OK;

@@ -1506,9 +1506,12 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
     hipLaunchKernelGGL(pos_iota_kernel, dim3(g), dim3(256), 0, st, pcomp, n);  // comp = own position
     auto round_seed = [&](int round) {
         const int prev = (round > 0 && ctx->boruvka_seed) ? 1 : 0;
-        const int K = kl ? kl->K : 0;
+        // the lists stop paying once components outgrow them (their points are then all
+        // inside the component): seed from them only in the first list_rounds rounds
+        const int K = (kl && round < ctx->leaf_list_rounds) ? kl->K : 0;
         if (!prev && K == 0) {
             if (round > 0) hipLaunchKernelGGL(fill_inf_kernel, dim3(g), dim3(256), 0, st, best_w, n);
+            if (kl && kl->done) HIP_CHECK(hipMemsetAsync(kl->done, 0, (size_t)n, st));  // no exact seeds
             return;
         }
         const int gs = (int)std::min<int64_t>(ceil_div(n, 256), 2048);
@@ -1732,7 +1735,11 @@ static void exact_leaf_impl(hdb_ctx *ctx, const double *X, int64_t n, int min_pt
 template <int D>
 static bool exact_leaf_k(hdb_ctx *ctx, const double *X, int64_t n, int min_pts, int semantics, double *core,
                          int self_edges, int32_t *va, int32_t *vb, double *w) {
-    switch (pick_kc(min_pts - 1)) {
+    // list length: >= minPts-1; longer lists make more round-0/1 seeds provably exact
+    // (measured at d = 3, 1M blobs: K = 7 cuts the scans by 1.6 ms for +0.7 ms of k-NN)
+    const int seed_k = ctx->leaf_seed_k >= 0 ? ctx->leaf_seed_k : (D <= 3 ? 7 : 0);
+    const int k = min_pts - 1 > seed_k ? min_pts - 1 : seed_k;
+    switch (pick_kc(k)) {
     case 1: exact_leaf_impl<D, 1>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); return true;
     case 3: exact_leaf_impl<D, 3>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); return true;
     case 7: exact_leaf_impl<D, 7>(ctx, X, n, min_pts, semantics, core, self_edges, va, vb, w); return true;

@@ -26,7 +26,8 @@ def eq(a, b):
 
 @contextlib.contextmanager
 def options(ctx, **kw):
-    defaults = {"knn_tree": 1, "knn_tree_min_n": 8192, "knn_fp32_screen": 1, "count_evals": 0}
+    defaults = {"knn_tree": 1, "knn_tree_min_n": 8192, "knn_fp32_screen": 1, "count_evals": 0,
+                "leaf_seed_k": -1, "leaf_list_rounds": 2, "boruvka_seed": 1}
     try:
         for k, v in kw.items():
             ctx.set_option(k, v)
@@ -188,3 +189,21 @@ def test_exact_mst_device_full_size(star):
     b = star.constructMSTBoruvka(t, ref_core, False)
     assert torch.equal(g.getEges(), b.getEges())
     assert torch.equal(g.getVerticeA(), b.getVerticeA()) and torch.equal(g.getVericeB(), b.getVericeB())
+
+
+@pytest.mark.parametrize("d", [2, 3, 8])
+def test_exact_mst_seeding_options_equal(ctx, star, d):
+    """Every seeding knob (list length, rounds seeded from the lists, previous-round seeds and
+    their carried bounds) changes only which lanes search, never the MST: edge for edge
+    equal to the plain constructMSTBoruvka on the same cores (tie-heavy rounded blobs)."""
+    X = np.round(blobs(20000, d, 12, 7 * d), 1)
+    core, _ = star.exactMST(X, 4, None, 2, selfEdges=False)
+    ref = _sorted_edges(star.constructMSTBoruvka(X, core, False))
+    for kw in ({}, dict(leaf_seed_k=0), dict(leaf_seed_k=7, leaf_list_rounds=64),
+               dict(leaf_seed_k=15, leaf_list_rounds=1), dict(leaf_list_rounds=0),
+               dict(boruvka_seed=0), dict(boruvka_seed=0, leaf_list_rounds=1)):
+        with options(ctx, **kw):
+            c2, g = star.exactMST(X, 4, None, 2, selfEdges=False)
+        assert eq(c2, core), kw
+        for u, v in zip(_sorted_edges(g), ref):
+            assert eq(np.asarray(u, dtype=np.float64), np.asarray(v, dtype=np.float64)), (d, kw)
