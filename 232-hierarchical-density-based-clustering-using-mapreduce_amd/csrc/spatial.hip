@@ -200,6 +200,12 @@ __global__ void build_recs_kernel(const double *__restrict__ X, const double *__
 // tag: a leaf visit skips a sub-group no lane needs (finer culling, same wave shape).
 constexpr int SG = 16;
 constexpr int NSG = BT / SG;
+#ifndef HDB_LEAF_PREFETCH
+#define HDB_LEAF_PREFETCH 1
+#endif
+#ifndef HDB_BOR_WPE  // waves per EU the D <= 3 Boruvka scan is compiled for
+#define HDB_BOR_WPE 4
+#endif
 
 template <int D>
 __global__ void tile_box_kernel(const Rec<D> *__restrict__ recs, int64_t n, double *__restrict__ tlo,
@@ -521,7 +527,7 @@ __device__ __forceinline__ void publish_min(unsigned long long *arr, int32_t c, 
 }
 
 template <int D, bool STATS>
-__global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
+__global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
                                                           Bvh bvh, unsigned long long *__restrict__ comp_w,
                                                           double *__restrict__ best_w, double *__restrict__ best_s,
                                                           int32_t *__restrict__ best_lo, int32_t *__restrict__ best_hi,
@@ -629,6 +635,30 @@ __global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(cons
     if (lane == 0) stk[0] = ((bvh.levels - 1) << 26) | 0;
     sp = 1;
     int visits = 0;
+#if HDB_LEAF_PREFETCH
+    static_assert(NSG * D <= 64, "one group-box element per lane");
+    int32_t pf_code = -1;  // stack code of the leaf held in the pf_* registers
+    LRec<D> pf_rec;
+    double pf_l = 0, pf_h = 0;
+    int32_t pf_tg = -1;
+    auto issue_leaf = [&](int64_t tile, LRec<D> &r, double &gl, double &gh, int32_t &gt) {
+        r = fetch_rec<D>(recs, n, tile * BT + lane);
+        const int e = lane < NSG * D - 1 ? lane : NSG * D - 1;  // clamped: unconditional loads
+        gl = bvh.slo[tile * NSG * D + e];
+        gh = bvh.shi[tile * NSG * D + e];
+        gt = bvh.stag[tile * NSG + (lane < NSG - 1 ? lane : NSG - 1)];
+    };
+    auto commit_leaf = [&](const LRec<D> &r, double gl, double gh, int32_t gt) {  // as stage_boxes<D, NSG>
+        __builtin_amdgcn_wave_barrier();
+        if (lane < NSG * D) {
+            bxs[lane] = gl;
+            bxs[NSG * D + lane] = gh;
+        }
+        if (lane < NSG) bxt[lane] = gt;
+        cand[lane] = r;
+        __builtin_amdgcn_wave_barrier();
+    };
+#endif
     while (sp > 0) {
         __builtin_amdgcn_wave_barrier();
         const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
@@ -652,11 +682,36 @@ __global__ __launch_bounds__(256, (D <= 3 ? 5 : 1)) void boruvka_bvh_kernel(cons
         // vector load together with the group boxes, then staged in LDS.
         n_leaf++;
         bool found = false;
+#if HDB_LEAF_PREFETCH
+        {
+            // a leaf pushes nothing, so the next pop is the entry now on top of the stack: when
+            // that is a leaf too, its loads were issued while this wave evaluated the previous
+            // leaf (one dependent round trip less per leaf run)
+            LRec<D> r;
+            double gl, gh;
+            int32_t gt;
+            if (code == pf_code) {
+                r = pf_rec, gl = pf_l, gh = pf_h, gt = pf_tg;
+            } else {
+                issue_leaf(idx, r, gl, gh, gt);
+            }
+            commit_leaf(r, gl, gh, gt);
+            pf_code = -1;
+            if (sp > 0) {
+                const int32_t nc = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
+                if ((nc >> 26) == 0) {
+                    issue_leaf(nc & ((1 << 26) - 1), pf_rec, pf_l, pf_h, pf_tg);
+                    pf_code = nc;
+                }
+            }
+        }
+#else
         const LRec<D> mine = fetch_rec<D>(recs, n, idx * BT + lane);
         stage_boxes<D, NSG>(bvh.slo + idx * NSG * D, bvh.shi + idx * NSG * D, bvh.stag + idx * NSG, NSG, bxs, bxt,
                             lane);
         cand[lane] = mine;  // staged now: the record's registers die before the culling
         __builtin_amdgcn_wave_barrier();
+#endif
         auto gneeds = [&](int gi) -> bool {
             double a[D], bb[D];
             staged_box<D, NSG>(bxs, gi, a, bb);
