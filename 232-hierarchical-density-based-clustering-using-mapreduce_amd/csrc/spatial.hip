@@ -203,6 +203,9 @@ constexpr int NSG = BT / SG;
 #ifndef HDB_LEAF_PREFETCH
 #define HDB_LEAF_PREFETCH 1
 #endif
+#ifndef HDB_K1T_PREFETCH  // the same prefetch in K1t: off -- 82 -> 104 VGPRs drops K1t to 4
+#define HDB_K1T_PREFETCH 0  // waves/SIMD and costs more than it hides (2.0 -> 2.23 ms)
+#endif
 #ifndef HDB_BOR_WPE  // waves per EU the D <= 3 Boruvka scan is compiled for
 #define HDB_BOR_WPE 4
 #endif
@@ -368,6 +371,39 @@ __device__ __forceinline__ void staged_box(const double *sb, int k, double (&a)[
         b[c] = sb[NB * D + k * D + c];
     }
 }
+
+#if HDB_LEAF_PREFETCH
+// A leaf tile's records and group boxes held in registers (one element per lane), so a leaf
+// can be loaded while the wave still evaluates the previous one.  commit == stage_boxes<D,
+// NSG> + the cand[] staging.
+template <int D>
+struct LeafRegs {
+    LRec<D> r;
+    double gl = 0, gh = 0;
+    int32_t gt = -1;
+};
+template <int D>
+__device__ __forceinline__ void leaf_issue(const Rec<D> *__restrict__ recs, int64_t n, const Bvh &bvh, int64_t tile,
+                                           int lane, LeafRegs<D> &L) {
+    static_assert(NSG * D <= 64, "one group-box element per lane");
+    L.r = fetch_rec<D>(recs, n, tile * BT + lane);
+    const int e = lane < NSG * D - 1 ? lane : NSG * D - 1;  // clamped: unconditional loads
+    L.gl = bvh.slo[tile * NSG * D + e];
+    L.gh = bvh.shi[tile * NSG * D + e];
+    L.gt = bvh.stag[tile * NSG + (lane < NSG - 1 ? lane : NSG - 1)];
+}
+template <int D>
+__device__ __forceinline__ void leaf_commit(const LeafRegs<D> &L, LRec<D> *cand, double *bxs, int32_t *bxt, int lane) {
+    __builtin_amdgcn_wave_barrier();
+    if (lane < NSG * D) {
+        bxs[lane] = L.gl;
+        bxs[NSG * D + lane] = L.gh;
+    }
+    if (lane < NSG) bxt[lane] = L.gt;
+    cand[lane] = L.r;
+    __builtin_amdgcn_wave_barrier();
+}
+#endif
 
 // The BVH level table (offset and node count per level, as bvh_shape) rebuilt per wave in
 // LDS from ntiles: reading Bvh::off/cnt with a dynamic level index from the kernel arguments
@@ -636,28 +672,8 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
     sp = 1;
     int visits = 0;
 #if HDB_LEAF_PREFETCH
-    static_assert(NSG * D <= 64, "one group-box element per lane");
-    int32_t pf_code = -1;  // stack code of the leaf held in the pf_* registers
-    LRec<D> pf_rec;
-    double pf_l = 0, pf_h = 0;
-    int32_t pf_tg = -1;
-    auto issue_leaf = [&](int64_t tile, LRec<D> &r, double &gl, double &gh, int32_t &gt) {
-        r = fetch_rec<D>(recs, n, tile * BT + lane);
-        const int e = lane < NSG * D - 1 ? lane : NSG * D - 1;  // clamped: unconditional loads
-        gl = bvh.slo[tile * NSG * D + e];
-        gh = bvh.shi[tile * NSG * D + e];
-        gt = bvh.stag[tile * NSG + (lane < NSG - 1 ? lane : NSG - 1)];
-    };
-    auto commit_leaf = [&](const LRec<D> &r, double gl, double gh, int32_t gt) {  // as stage_boxes<D, NSG>
-        __builtin_amdgcn_wave_barrier();
-        if (lane < NSG * D) {
-            bxs[lane] = gl;
-            bxs[NSG * D + lane] = gh;
-        }
-        if (lane < NSG) bxt[lane] = gt;
-        cand[lane] = r;
-        __builtin_amdgcn_wave_barrier();
-    };
+    int32_t pf_code = -1;  // stack code of the leaf held in pf
+    LeafRegs<D> pf;
 #endif
     while (sp > 0) {
         __builtin_amdgcn_wave_barrier();
@@ -687,20 +703,17 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
             // a leaf pushes nothing, so the next pop is the entry now on top of the stack: when
             // that is a leaf too, its loads were issued while this wave evaluated the previous
             // leaf (one dependent round trip less per leaf run)
-            LRec<D> r;
-            double gl, gh;
-            int32_t gt;
-            if (code == pf_code) {
-                r = pf_rec, gl = pf_l, gh = pf_h, gt = pf_tg;
-            } else {
-                issue_leaf(idx, r, gl, gh, gt);
-            }
-            commit_leaf(r, gl, gh, gt);
+            LeafRegs<D> cur;
+            if (code == pf_code)
+                cur = pf;
+            else
+                leaf_issue<D>(recs, n, bvh, idx, lane, cur);
+            leaf_commit<D>(cur, cand, bxs, bxt, lane);
             pf_code = -1;
             if (sp > 0) {
                 const int32_t nc = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
                 if ((nc >> 26) == 0) {
-                    issue_leaf(nc & ((1 << 26) - 1), pf_rec, pf_l, pf_h, pf_tg);
+                    leaf_issue<D>(recs, n, bvh, nc & ((1 << 26) - 1), lane, pf);
                     pf_code = nc;
                 }
             }
@@ -1198,14 +1211,39 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
     auto needs_vals = [&](const double (&a)[D], const double (&b)[D], int32_t) -> bool {
         return valid & (box_lb2v<D>(mx, a, b) < buf[K - 1]);
     };
+    int sp = 0;
+#if HDB_LEAF_PREFETCH && HDB_K1T_PREFETCH
+    int64_t pf_tile = -1;  // leaf held in pf (issued while the previous leaf was evaluated)
+    LeafRegs<D> pf;
+#endif
     auto scan_leaf = [&](int64_t tile, bool own) {
         // the tile's 64 records (one coalesced vector load) and group boxes (cooperative
         // staging), one round trip; the records are staged in LDS for broadcast reads
+#if HDB_LEAF_PREFETCH && HDB_K1T_PREFETCH
+        {
+            LeafRegs<D> cur;
+            if (tile == pf_tile)
+                cur = pf;
+            else
+                leaf_issue<D>(recs, n, bvh, tile, lane, cur);
+            leaf_commit<D>(cur, cand, bxs, bxt, lane);
+            // a leaf pushes nothing: when the stack top is a leaf, it is the next pop
+            pf_tile = -1;
+            if (sp > 0) {
+                const int32_t nc = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
+                if ((nc >> 26) == 0 && (nc & ((1 << 26) - 1)) != t) {
+                    pf_tile = nc & ((1 << 26) - 1);
+                    leaf_issue<D>(recs, n, bvh, pf_tile, lane, pf);
+                }
+            }
+        }
+#else
         const LRec<D> mine = fetch_rec<D>(recs, n, tile * BT + lane);
         stage_boxes<D, NSG>(bvh.slo + tile * NSG * D, bvh.shi + tile * NSG * D, bvh.stag + tile * NSG, NSG, bxs, bxt,
                             lane);
         cand[lane] = mine;  // staged now: the record's registers die before the culling
         __builtin_amdgcn_wave_barrier();
+#endif
         auto gneeds = [&](int gi) -> bool {
             double a[D], b[D];
             staged_box<D, NSG>(bxs, gi, a, b);
@@ -1243,7 +1281,6 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict_
     if (lane < 2 * D) q_s[w][lane] = lane < D ? bvh.lo[t * D + lane] : bvh.hi[t * D + lane - D];
     __builtin_amdgcn_wave_barrier();
     level_table(ntiles, off_s, cnt_s, lane);
-    int sp = 0;
     if (lane == 0) stk[0] = ((bvh.levels - 1) << 26) | 0;
     sp = 1;
     while (sp > 0) {
