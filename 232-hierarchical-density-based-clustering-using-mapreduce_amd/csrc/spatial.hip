@@ -206,6 +206,9 @@ constexpr int NSG = BT / SG;
 #ifndef HDB_K1T_PREFETCH  // the same prefetch in K1t: off -- 82 -> 104 VGPRs drops K1t to 4
 #define HDB_K1T_PREFETCH 0  // waves/SIMD and costs more than it hides (2.0 -> 2.23 ms)
 #endif
+#ifndef HDB_K1T_WPE  // waves per EU the D <= 3 K1t is compiled for (82 VGPRs free-running: 5)
+#define HDB_K1T_WPE 5
+#endif
 #ifndef HDB_BOR_WPE  // waves per EU the D <= 3 Boruvka scan is compiled for
 #define HDB_BOR_WPE 4
 #endif
@@ -1166,7 +1169,7 @@ __global__ __launch_bounds__(256) void round_seed_kernel(const Rec<D> *__restric
 // wave-uniform broadcast reads, and each lane evaluates the exact FP64 squared distance in
 // the reference's order and feeds the register top-K network.
 template <int D, int K, bool IDX, bool STATS>
-__global__ __launch_bounds__(256) void knn_tree_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
+__global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
                                                        Bvh bvh, int excl, double *__restrict__ lists,
                                                        int32_t *__restrict__ nb_pos, double *__restrict__ nb_s,
                                                        int pop_test, unsigned long long *__restrict__ stats) {
