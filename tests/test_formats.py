@@ -121,3 +121,20 @@ def test_local_mst_parse_errors(pkg):
         pkg.parse_local_mst("")  # "".split("\n") == [""] -> data[1] throws
     va, vb, w, *_ = pkg.parse_local_mst("1 2 1.0E-5 0 0 0\n3 4 5.0 0 0 1\n\n")
     assert va.tolist() == [1, 3] and w.tolist() == [1e-5, 5.0]
+
+
+@pytest.mark.gpu
+def test_dataset_to_local_mst_text_on_device(pkg, oracle):
+    """The reference's own data path end to end: dataset.txt -> MapperDataset_github points
+    -> exact leaf MST on the GPU -> CreateLocalMST text -> UnionFindReducer parse: the
+    parsed records equal the MST (and the oracle's Prim weights)."""
+    X = pkg.read_dataset(os.path.join(GOLDEN, "iris_dataset.txt"), strict=True)
+    core, mst = pkg.HDBSCANStar().exactMST(X, 4, None, pkg.CORE_EXCL_SELF, True)
+    va, vb, w = (np.asarray(a) for a in (mst.getVerticeA(), mst.getVericeB(), mst.getEges()))
+    text = pkg.format_local_mst(va, vb, w)
+    assert text == OF.format_local_mst(va, vb, w)
+    pa, pb, pw, *_ = pkg.parse_local_mst(text)
+    assert np.array_equal(pa, va) and np.array_equal(pb, vb) and np.array_equal(pw, w)
+    ref_core = oracle.core_distances(X, 4, semantics=oracle.EXCL_SELF)
+    _, _, rw = oracle.prim_mst(X, ref_core, self_edges=False)
+    assert np.array_equal(np.sort(pw[: X.shape[0] - 1]), np.sort(rw))
