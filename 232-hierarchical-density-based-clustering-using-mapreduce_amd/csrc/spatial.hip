@@ -1609,7 +1609,7 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             if (kl && kl->done) HIP_CHECK(hipMemsetAsync(kl->done, 0, (size_t)n, st));  // no exact seeds
             return;
         }
-        const int gs = (int)std::min<int64_t>(ceil_div(n, 256), 1 << 20);  // one lane per point: the random neighbour reads need all the parallelism
+        const int gs = (int)std::min<int64_t>(ceil_div(n, 256), 2048);
 #define ROUND_SEED(KK)                                                                                                 \
     case KK:                                                                                                           \
         hipLaunchKernelGGL((round_seed_kernel<D, KK>), dim3(gs), dim3(256), 0, st, recs, pcomp, n, prev,              \
