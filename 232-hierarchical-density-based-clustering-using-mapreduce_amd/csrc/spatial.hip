@@ -1609,7 +1609,10 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             if (kl && kl->done) HIP_CHECK(hipMemsetAsync(kl->done, 0, (size_t)n, st));  // no exact seeds
             return;
         }
-        const int gs = (int)std::min<int64_t>(ceil_div(n, 256), 2048);
+#ifndef HDB_SEED_MAX_BLOCKS
+#define HDB_SEED_MAX_BLOCKS 2048
+#endif
+        const int gs = (int)std::min<int64_t>(ceil_div(n, 256), HDB_SEED_MAX_BLOCKS);
 #define ROUND_SEED(KK)                                                                                                 \
     case KK:                                                                                                           \
         hipLaunchKernelGGL((round_seed_kernel<D, KK>), dim3(gs), dim3(256), 0, st, recs, pcomp, n, prev,              \
