@@ -110,11 +110,9 @@ suffix:
     if (q < e && (*q == 'f' || *q == 'F' || *q == 'd' || *q == 'D')) ++q;
     if (q != e) return false;
     std::string s(b, num_end);
-    // a float suffix makes Java round to float first (Float.parseDouble semantics)
-    bool as_float = num_end < e && (*num_end == 'f' || *num_end == 'F');
-    double v = strtod_l(s.c_str(), nullptr, c_locale());
-    if (as_float) v = (double)(float)v;
-    *out = v;
+    // a type suffix (f/F/d/D) does not influence the result of Double.parseDouble (its
+    // javadoc; FloatingDecimal returns the same digits' doubleValue)
+    *out = strtod_l(s.c_str(), nullptr, c_locale());
     return true;
 }
 
@@ -167,22 +165,51 @@ int java_double_to_string(double v, char *buf) {
         strcpy(o, "0.0");
         return (int)(o - buf) + 3;
     }
-    // shortest p in [1, 17] whose correctly rounded p-digit decimal parses back to v; the
-    // property is monotone in p, so bisect
+    // shortest p in [1, 17] with a p-digit decimal that parses back to v.  The nearest
+    // p-digit decimal (%.*e) is the candidate; at a power of two the rounding interval is
+    // asymmetric (the lower gap is half the upper), so when the nearest one misses, the
+    // next p-digit decimal upwards (the wider side) can still be inside: try it too.
     char tmp[40];
-    int lo = 1, hi = 17;
-    while (lo < hi) {
-        int mid = (lo + hi) / 2;
-        snprintf(tmp, sizeof tmp, "%.*e", mid - 1, v);
-        if (strtod_l(tmp, nullptr, c_locale()) == v)
-            hi = mid;
-        else
-            lo = mid + 1;
-    }
+    auto fits = [&](int p, char *cand) {
+        snprintf(cand, 40, "%.*e", p - 1, v);
+        if (strtod_l(cand, nullptr, c_locale()) == v) return true;
+        double m, x = v;
+        int ex = 0;
+        m = std::frexp(x, &ex);
+        if (m != 0.5) return false;  // not a power of two: the interval is symmetric
+        // bump the last digit of the nearest candidate by one unit
+        char dg[24];
+        int nd = 0;
+        const char *t = cand;
+        for (; *t && *t != 'e'; ++t)
+            if (is_digit(*t)) dg[nd++] = *t;
+        int E = atoi(t + 1);
+        int i = nd - 1;
+        while (i >= 0 && dg[i] == '9') dg[i--] = '0';
+        if (i < 0) {  // 9.99 -> 10.0: one more leading digit
+            dg[0] = '1';
+            for (int j = 1; j < nd; ++j) dg[j] = '0';
+            ++E;
+        } else {
+            ++dg[i];
+        }
+        char up[40], *o = up;
+        *o++ = dg[0];
+        if (nd > 1) {
+            *o++ = '.';
+            for (int j = 1; j < nd; ++j) *o++ = dg[j];
+        }
+        sprintf(o, "e%d", E);
+        if (strtod_l(up, nullptr, c_locale()) != v) return false;
+        strcpy(cand, up);
+        return true;
+    };
+    int lo = 1;
+    while (lo < 17 && !fits(lo, tmp)) ++lo;
     // Java's rule when one digit suffices: the closest decimal of length 1 or 2, i.e. the
     // correctly rounded 2-digit one (4.9E-324, not 5.0E-324)
     if (lo < 2) lo = 2;
-    snprintf(tmp, sizeof tmp, "%.*e", lo - 1, v);
+    if (!fits(lo, tmp)) snprintf(tmp, sizeof tmp, "%.*e", lo - 1, v);
     char dig[20];
     int nd = 0;
     const char *t = tmp;
@@ -319,15 +346,21 @@ int hdb_parse_mst_records(const char *text, int64_t len, int32_t *va, int32_t *v
     int64_t i = 0;
     for (auto &ln : lines) {
         java_split(ln.first, ln.second, ' ', f);
-        if (f.size() < 6)  // data[k] on a short split
-            return fail(HDB_EREF_OOB, "hdb_parse_mst_records: record %lld has %zu fields", (long long)i, f.size());
-        int32_t a, b, f1, f2, nd;
-        double ww;
-        if (!java_parse_int(f[0].first, f[0].second, &a) || !java_parse_int(f[1].first, f[1].second, &b) ||
-            !java_parse_double(f[2].first, f[2].second, &ww) || !java_parse_int(f[3].first, f[3].second, &f1) ||
-            !java_parse_int(f[4].first, f[4].second, &f2) || !java_parse_int(f[5].first, f[5].second, &nd))
-            return fail(HDB_EREF_NUMBER_FORMAT, "hdb_parse_mst_records: record %lld: \"%.*s\"", (long long)i,
-                        (int)(ln.second - ln.first), ln.first);
+        // UnionFindReducer.java:26-31 reads data[0] .. data[5] in order: a bad early field
+        // throws NumberFormatException before a missing later index throws
+        // ArrayIndexOutOfBoundsException
+        int32_t iv[6] = {0, 0, 0, 0, 0, 0};
+        double ww = 0.0;
+        for (size_t k = 0; k < 6; ++k) {
+            if (k >= f.size())
+                return fail(HDB_EREF_OOB, "hdb_parse_mst_records: record %lld has %zu fields", (long long)i, f.size());
+            const bool ok = k == 2 ? java_parse_double(f[k].first, f[k].second, &ww)
+                                   : java_parse_int(f[k].first, f[k].second, &iv[k]);
+            if (!ok)
+                return fail(HDB_EREF_NUMBER_FORMAT, "hdb_parse_mst_records: record %lld: For input string: \"%.*s\"",
+                            (long long)i, (int)(f[k].second - f[k].first), f[k].first);
+        }
+        const int32_t a = iv[0], b = iv[1], f1 = iv[3], f2 = iv[4], nd = iv[5];
         if (fill) {
             va[i] = a, vb[i] = b, w[i] = ww;
             if (fake1) fake1[i] = f1;

@@ -12,9 +12,10 @@ oracle for the parity tests):
   level loop (Main.java:107)   subsets grouped by key, ascending (D5)
   leaves  (FirstStep.java:104-120)  subsets <= processing_units (or forced, D9): cumulative
           core distances + Prim with self edges over the rows in ascending global id, one
-          batched launch for all leaves <= LEAF_PRIM_MAX points; larger forced leaves use
-          hdb_exact_mst: the same cores + Boruvka on one index (exact weights; topology differs
-          from Prim only on ties)
+          batched call for all leaves <= LEAF_PRIM_MAX points (and for any size when
+          exact_prim_leaves is set or K2b does not apply: other metrics, other d); larger
+          forced leaves use hdb_exact_mst: the same cores + Boruvka on one index (exact
+          weights; topology differs from Prim only on ties)
   big subsets: D2 samples -> keyed nearest sample (FirstStep.java:74-85, D3) -> bulk
           CombineStep (D5 fold order) -> per subset LocalModelReduceByKey (D4) -> partition
           induction (Main.java:272-289, including the in-place relabel) -> LabelClassification
@@ -29,7 +30,14 @@ import numpy as np
 from . import _capi as A
 from .hdbscanstar import metric_of
 
-LEAF_PRIM_MAX = 4096  # leaves up to this size run the exact reference Prim (batched)
+LEAF_PRIM_MAX = 65536  # leaves up to this size run the exact reference Prim (batched; one
+#                       workgroup per leaf <= 4096 points, one cooperative launch above)
+BORUVKA_DIMS = (1, 2, 3, 4, 8, 16)  # d with a K1t/K2b instantiation (csrc/spatial.hip)
+
+
+def boruvka_ok(metric: int, d: int, min_pts: int) -> bool:
+    """hdb_exact_mst's K2b path: Euclidean, d with an instantiation, 2 <= minPts <= 32."""
+    return metric == A.METRIC["euclidean"] and d in BORUVKA_DIMS and 2 <= min_pts <= 32
 
 
 def sample_ids(n_key: int, k: float, samples_per_subset, seed: int, iteration: int, key: int):
@@ -46,7 +54,7 @@ class MRHDBSCANStar:
 
     def __init__(self, minPts=4, minClSize=4, processing_units=50, k=0.2, samples_per_subset=None,
                  seed=20210101, distanceFunction=None, all_inter_edges=True, max_levels=64, ctx=None,
-                 device=0, flat_labels=True, profile=False):
+                 device=0, flat_labels=True, profile=False, exact_prim_leaves=False):
         self.minPts = minPts
         self.minClSize = minClSize
         self.processing_units = processing_units
@@ -60,6 +68,11 @@ class MRHDBSCANStar:
         self.ctx = ctx
         self.flat_labels = flat_labels
         self.profile = profile       # phase wall times (synchronising) in self.timings
+        # True: every leaf, however large, runs the reference Prim (the exact edge list of
+        # HDBSCANStar.constructMST, ties included; stepwise above 65,536 points).  False:
+        # forced leaves above LEAF_PRIM_MAX use Boruvka where it applies (same weights,
+        # topology may differ among equal-weight edges)
+        self.exact_prim_leaves = exact_prim_leaves
         self.timings = {}
         self._t0 = None
 
@@ -87,7 +100,10 @@ class MRHDBSCANStar:
         import torch
         out = []
         c = self._c()
-        small = [(k, r) for k, r in zip(keys, rows_list) if r.shape[0] <= LEAF_PRIM_MAX]
+        d = X.shape[1]
+        prim = lambda n: (n <= LEAF_PRIM_MAX or self.exact_prim_leaves
+                          or not boruvka_ok(self.metric, d, self.minPts))
+        small = [(k, r) for k, r in zip(keys, rows_list) if prim(r.shape[0])]
         if small:
             rows = torch.cat([r for _, r in small])
             sizes = np.array([r.shape[0] for _, r in small], np.int64)
@@ -113,8 +129,8 @@ class MRHDBSCANStar:
             if k in by_key:
                 out.append(by_key[k])
                 continue
-            # large forced leaf (D9): cumulative cores + exact MST (Boruvka: exact weights) in one
-            # call sharing one spatial index (hdb_exact_mst)
+            # large forced leaf (D9) where K2b applies: cumulative cores + exact MST (Boruvka:
+            # exact weights) in one call sharing one spatial index (hdb_exact_mst)
             Xl = X.index_select(0, r).contiguous()
             n = r.shape[0]
             ne = 2 * n - 1

@@ -50,9 +50,7 @@ def parse_double(s: str) -> float:
         v = float.fromhex(body)
     else:
         v = float(body.replace("Infinity", "inf"))
-    if suffix in ("f", "F"):
-        import struct
-        v = struct.unpack("f", struct.pack("f", v))[0]
+    # a type suffix does not influence the result (Double.parseDouble javadoc)
     return v
 
 
@@ -128,8 +126,10 @@ def parse_local_mst(text: str):
     out = []
     for ln in java_split(text, "\n"):
         data = java_split(ln, " ")
-        if len(data) < 6:
-            raise IndexError(len(data))
-        out.append((parse_int(data[0]), parse_int(data[1]), parse_double(data[2]), parse_int(data[3]),
-                    parse_int(data[4]), parse_int(data[5])))
+        rec = []
+        for k in range(6):  # UnionFindReducer.java:26-31: data[0..5] parsed in order
+            if k >= len(data):
+                raise IndexError(len(data))
+            rec.append(parse_double(data[k]) if k == 2 else parse_int(data[k]))
+        out.append(tuple(rec))
     return out

@@ -42,7 +42,7 @@ def sample_ids(n_key: int, k: float, samples_per_subset: int | None, seed: int, 
 
 
 def run(X, min_pts=4, min_cl_size=4, processing_units=50, k=0.2, samples_per_subset=None, seed=20210101,
-        metric="euclidean", all_inter_edges=True, max_levels=64):
+        metric="euclidean", all_inter_edges=True, max_levels=64, log=None):
     """Returns dict(edges=(va, vb, w) merged (stable, descending weight), levels=[...],
     leaf_of=np.array subset key of the leaf that processed each point, iterations)."""
     X = np.ascontiguousarray(X, np.float64)
@@ -69,6 +69,10 @@ def run(X, min_pts=4, min_cl_size=4, processing_units=50, k=0.2, samples_per_sub
                 big_keys.append(c)
         level = dict(iteration=iteration, leaves={c: members[c].shape[0] for c in leaf_keys},
                      big={c: members[c].shape[0] for c in big_keys}, labels={}, new_keys={})
+        if log:
+            log(f"level {iteration}: {len(leaf_keys)} leaves ({sum(level['leaves'].values())} pts, "
+                f"max {max(level['leaves'].values(), default=0)}), {len(big_keys)} big subsets "
+                f"({sum(level['big'].values())} pts)")
         # FirstStep leaf branch (FirstStep.java:104-120)
         leaf_edges = []
         for c in leaf_keys:

@@ -58,6 +58,26 @@ def test_parse_double_java_grammar(pkg):
             pkg.read_dataset(("1 " + s) if s else "1  2", strict=True)
 
 
+def test_parse_double_ignores_type_suffix(pkg):
+    """Double.parseDouble's javadoc: trailing type specifiers (1.0f, 1.0d) do not influence the
+    result -- "0.1f" is the double 0.1, not the float 0.1f widened."""
+    for s, v in [("0.1f", 0.1), ("0.1F", 0.1), ("0x1.999999999999ap-4F", 0.1), ("0.1d", 0.1),
+                 ("1.1f", 1.1), ("3.3e-3F", 3.3e-3)]:
+        assert OF.parse_double(s) == v, s
+        assert pkg.read_dataset(s + "\n", strict=True)[0, 0] == v, s
+
+
+def test_double_to_string_powers_of_two(pkg):
+    """At a power of two the rounding interval is asymmetric; the shortest digits can be a
+    decimal farther than the nearest one of that length (Python's repr finds them)."""
+    import math
+    for k in range(-1074, 1024):
+        v = math.ldexp(1.0, k)
+        s = pkg.double_to_string(v)
+        assert s == OF.double_to_string(v), (k, s)
+        assert OF.parse_double(s) == v
+
+
 def test_strict_split_semantics(pkg):
     """s.split(" "): trailing empty fields vanish, a doubled space is an empty field, tabs are
     not separators (-> NumberFormatException on Skin's TAB lines without D1)."""
@@ -117,8 +137,20 @@ def test_local_mst_parse_errors(pkg):
         pkg.parse_local_mst("1 2 0.5 0 0 x")
     with pytest.raises(pkg.NumberFormatException):
         pkg.parse_local_mst("1 2 0.5 0 0 2147483648")
+    # UnionFindReducer.java:26-31 parses data[0..5] in order: a bad early field throws
+    # NumberFormatException before a missing index is reached
+    with pytest.raises(pkg.NumberFormatException):
+        pkg.parse_local_mst("")  # "".split("\n") == [""] -> Integer.parseInt("") throws
+    with pytest.raises(OF.NumberFormatException):
+        OF.parse_local_mst("")
+    with pytest.raises(pkg.NumberFormatException):
+        pkg.parse_local_mst("1 2 x")  # data[2] throws before data[3] is read
+    with pytest.raises(OF.NumberFormatException):
+        OF.parse_local_mst("1 2 x")
     with pytest.raises(pkg.ArrayIndexOutOfBoundsException):
-        pkg.parse_local_mst("")  # "".split("\n") == [""] -> data[1] throws
+        pkg.parse_local_mst("1 2 0.5")
+    with pytest.raises(IndexError):
+        OF.parse_local_mst("1 2 0.5")
     va, vb, w, *_ = pkg.parse_local_mst("1 2 1.0E-5 0 0 0\n3 4 5.0 0 0 1\n\n")
     assert va.tolist() == [1, 3] and w.tolist() == [1e-5, 5.0]
 

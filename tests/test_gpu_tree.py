@@ -207,3 +207,51 @@ def test_exact_mst_seeding_options_equal(ctx, star, d):
         assert eq(c2, core), kw
         for u, v in zip(_sorted_edges(g), ref):
             assert eq(np.asarray(u, dtype=np.float64), np.asarray(v, dtype=np.float64)), (d, kw)
+
+
+def _spanning_tree(va, vb, n):
+    """Host union-find: the n-1 edges connect all n points without a cycle."""
+    p = np.arange(n)
+
+    def find(x):
+        while p[x] != x:
+            p[x] = p[p[x]]
+            x = p[x]
+        return x
+    assert va.shape[0] == n - 1
+    for a, b in zip(va.tolist(), vb.tolist()):
+        ra, rb = find(a), find(b)
+        assert ra != rb, "cycle"
+        p[rb] = ra
+    return True
+
+
+def test_exact_mst_1m_is_spanning_tree_with_prim_weights(star):
+    """C2 at full size (1M x 3) checked independently of K2b: the edges form a spanning tree
+    of the 1M points and the sorted weights equal those of the GPU stepwise reference Prim
+    (prim_step_kernel, HDBSCANStar.java:124-205, bit-exact against the oracle up to 60k),
+    which shares no code with the Boruvka path but the distance functor."""
+    import time
+    import torch
+    t = torch.from_numpy(blobs(1_000_000, 3, 20, 1)).cuda()
+    core, g = star.exactMST(t, 4, None, 2, selfEdges=False)
+    va, vb = g.getVerticeA().cpu().numpy(), g.getVericeB().cpu().numpy()
+    assert _spanning_tree(va, vb, 1_000_000)
+    t0 = time.perf_counter()
+    p = star.constructMST(t, core, False)
+    torch.cuda.synchronize()
+    print(f"stepwise Prim 1M: {time.perf_counter() - t0:.1f} s")
+    assert torch.equal(torch.sort(g.getEges())[0], torch.sort(p.getEges())[0])
+
+
+def test_exact_mst_full_skin_weights_equal_prim(star):
+    """All 245,057 Skin rows (max multiplicity 1,598: zero-weight ties everywhere), live
+    cumulative cores: K2b's sorted weights equal the GPU reference Prim's and its edges form
+    a spanning tree."""
+    import torch
+    X = torch.from_numpy(load_skin()).cuda()
+    n = X.shape[0]
+    core, g = star.exactMST(X, 4, None, 0, selfEdges=False)
+    assert _spanning_tree(g.getVerticeA().cpu().numpy(), g.getVericeB().cpu().numpy(), n)
+    p = star.constructMST(X, core, False)
+    assert torch.equal(torch.sort(g.getEges())[0], torch.sort(p.getEges())[0])
