@@ -435,26 +435,13 @@ int hdb_flat_labels(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, const do
     }
     return guarded(ctx, [&] {
         if (ne < 0 || n < 0 || (ne > 0 && (!va || !vb || !w)) || (n > 0 && !labels)) HDB_THROW(HDB_EINVAL, "bad arguments");
-        // host algorithm: bring device inputs over once
-        auto host = [&](const void *p, size_t bytes, std::vector<char> &buf) -> const void * {
-            if (!p || !is_device_ptr(p)) return p;
-            buf.resize(bytes);
-            HIP_CHECK(hipMemcpyAsync(buf.data(), p, bytes, hipMemcpyDeviceToHost, ctx->stream));
-            return buf.data();
-        };
-        std::vector<char> ba, bb, bw;
-        const int32_t *ha = (const int32_t *)host(va, sizeof(int32_t) * (size_t)ne, ba);
-        const int32_t *hb = (const int32_t *)host(vb, sizeof(int32_t) * (size_t)ne, bb);
-        const double *hw = (const double *)host(w, sizeof(double) * (size_t)ne, bw);
-        HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        const bool dev_out = labels && is_device_ptr(labels);
-        std::vector<int32_t> hl(dev_out ? (size_t)n : 0);
-        int32_t *out = dev_out ? hl.data() : labels;
-        flat_labels_host(ha, hb, hw, ne, n, min_cl_size, out, n_clusters);
-        if (dev_out) {
-            HIP_CHECK(hipMemcpyAsync(labels, hl.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
-            HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        }
+        // device algorithm (K6, flat.hip); host arrays are staged
+        Stager sg(ctx);
+        const int32_t *da = sg.in(va, (size_t)ne), *db = sg.in(vb, (size_t)ne);
+        const double *dw = sg.in(w, (size_t)ne);
+        int32_t *dl = sg.out(labels, (size_t)std::max<int64_t>(n, 0));
+        flat_labels_device(ctx, da, db, dw, ne, n, min_cl_size, dl, n_clusters);
+        sg.finish();
     });
 }
 

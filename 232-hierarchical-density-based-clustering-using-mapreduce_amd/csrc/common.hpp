@@ -54,7 +54,7 @@ struct hdb_ctx {
     std::vector<hdb::TimedLaunch> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, std::pair<double, int64_t>> acc;
-    hdb::Arena arenas[8];
+    hdb::Arena arenas[12];
     int64_t *pinned = nullptr;  // pinned_words(): async device -> host counters
     int num_cus = 256;
     bool force_fp64 = false;  // disable the FP32 screen in K1 (A/B and tests)
@@ -77,7 +77,10 @@ struct hdb_ctx {
 namespace hdb {
 
 // scratch slot ids
-enum { A_STAGE_IN = 0, A_STAGE_OUT = 1, A_WORK0 = 2, A_WORK1 = 3, A_WORK2 = 4, A_WORK3 = 5, A_PAD = 6, A_SORT = 7 };
+enum {
+    A_STAGE_IN = 0, A_STAGE_OUT = 1, A_WORK0 = 2, A_WORK1 = 3, A_WORK2 = 4, A_WORK3 = 5, A_PAD = 6, A_SORT = 7,
+    A_FLAT0 = 8, A_FLAT1 = 9, A_FLAT_TMP = 10
+};
 
 void *arena(hdb_ctx *ctx, int slot, size_t bytes);
 constexpr int PINNED_WORDS = 512;

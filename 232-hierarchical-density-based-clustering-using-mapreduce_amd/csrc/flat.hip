@@ -1,0 +1,726 @@
+// flat.hip -- K6: the global HDBSCAN* hierarchy and its flat (FOSC / excess-of-mass) labels
+// over a merged MST, on the device.  SURVEY.md §8(f) #1: the step the reference never
+// completes (Main.java:351-408); semantics = HDBSCANStar.java:208-625 (computeHierarchy-
+// AndClusterTree / propagateTree / findProminentClusters, commented out in the reference)
+// with the canonical rules of oracle/flat_labels.py and csrc/flat.cpp (the host algorithm this
+// must equal bit for bit): a tie group is removed at once (multi-way dendrogram nodes), one
+// stability term per (cluster, node) added in descending level order, FOSC children summed in
+// ascending smallest point id, labels 1..K by smallest point id, 0 = noise.
+//
+// Algorithm (all O(m) or O(m log m) data-parallel passes, m = n - 1 tree edges):
+//  1. compact the non-self edges, validate, rank them by ascending weight (the merged list
+//     arrives sorted descending: no sort; otherwise one radix sort);
+//  2. binary Kruskal (single-linkage) tree by rank divide and conquer: at depth j every rank
+//     block [lo, hi) splits into L = [lo, mid) and U = [mid, hi).  Endpoint labels name the
+//     component of F_{<lo} (the forest of ranks < lo) by its root edge, or the vertex itself
+//     -- such labels are unique across all blocks of a depth, so one union-find array serves
+//     them all.  The L edges are united; the lightest U edge touching an L component is the
+//     parent of that component's root (its largest L edge); U labels move to the new roots.
+//     The parent of edge e = the lightest edge on the boundary of C(e) (e plus the lighter
+//     edges connected to it), assigned at exactly one depth.  Component sizes and smallest
+//     ids ride along (|C(e)| and min id of C(e) per edge);
+//  3. equal-weight parent links merge edges into multi-way nodes (one node per component a
+//     tie group leaves); condensation is local: a node is reached iff it is the root or has
+//     >= minClSize points, a cluster starts at a valid child of a node with >= 2 valid
+//     children; pointer jumping (path halving) finds each node's cluster;
+//  4. per-cluster stability = sequential sum of its chain's terms in descending level (one
+//     radix sort groups the chains); FOSC over the (few) clusters on the host; labels by
+//     pointer jumping to the nearest selected ancestor.
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+#include <numeric>
+
+#include "common.hpp"
+#include "internal.hpp"
+#include "sort.hpp"
+
+namespace hdb {
+
+namespace {
+
+constexpr int32_t NONE = INT32_MAX;
+enum : int { FE_RANGE = 1, FE_NAN = 2, FE_CYCLE = 4, FE_ISOLATED = 8, FE_ROOTS = 16 };
+
+// --------------------------------------------------------------- union-find (parent >= id)
+// Roots hook under the LARGER id: a contracted label n + R that many edges share (a giant
+// component of the lower half) stays a root while singleton labels hook under it -- no CAS
+// contention on one entry.
+__device__ __forceinline__ int32_t uf_find(int32_t *uf, int32_t x) {
+    volatile int32_t *u = uf;
+    while (true) {
+        int32_t p = u[x];
+        if (p == x) return x;
+        int32_t g = u[p];
+        if (g == p) return p;
+        u[x] = g;  // path halving: g is an ancestor of x
+        x = g;
+    }
+}
+
+__device__ __forceinline__ bool uf_unite(int32_t *uf, int32_t a, int32_t b) {
+    while (true) {
+        a = uf_find(uf, a);
+        b = uf_find(uf, b);
+        if (a == b) return false;
+        if (a < b) {
+            int32_t t = a;
+            a = b;
+            b = t;
+        }
+        if (atomicCAS(&uf[b], b, a) == b) return true;  // b < a
+    }
+}
+
+// root of x in an "upward" forest (every pointer goes to a larger id, roots point to self),
+// compressing as it climbs
+__device__ __forceinline__ int32_t up_find(int32_t *up, int32_t x) {
+    volatile int32_t *u = up;
+    while (true) {
+        int32_t p = u[x];
+        if (p == x) return x;
+        int32_t g = u[p];
+        if (g == p) return p;
+        u[x] = g;
+        x = g;
+    }
+}
+
+// ------------------------------------------------------------------ 1. compact + rank
+__global__ void fl_mark(const int32_t *__restrict__ va, const int32_t *__restrict__ vb, const double *__restrict__ w,
+                        int64_t ne, int64_t n, int32_t *__restrict__ keep, int *__restrict__ err) {
+    int e = 0;
+    HDB_GRID_STRIDE(i, ne) {
+        int32_t a = va[i], b = vb[i];
+        int k = a != b;
+        keep[i] = k;
+        if (k) {
+            if (a < 0 || b < 0 || a >= n || b >= n) e |= FE_RANGE;
+            if (w[i] != w[i]) e |= FE_NAN;
+        }
+    }
+    if (e) atomicOr(err, e);
+}
+
+__global__ void fl_compact(const int32_t *__restrict__ va, const int32_t *__restrict__ vb, const double *__restrict__ w,
+                           int64_t ne, const int32_t *__restrict__ keep, const int32_t *__restrict__ pos,
+                           int64_t cap, int32_t *__restrict__ ca, int32_t *__restrict__ cb, double *__restrict__ cw,
+                           int64_t *__restrict__ m_out) {
+    HDB_GRID_STRIDE(i, ne) {
+        if (keep[i]) {
+            int32_t p = pos[i];
+            if (p < cap) {
+                ca[p] = va[i];
+                cb[p] = vb[i];
+                double x = w[i];
+                cw[p] = (x == 0.0) ? 0.0 : x;  // -0.0 ties +0.0 (== in the host algorithm)
+            }
+        }
+        if (i == ne - 1) *m_out = (int64_t)pos[i] + keep[i];
+    }
+}
+
+// bit 0: not descending, bit 1: not ascending
+__global__ void fl_order(const double *__restrict__ cw, const int64_t *__restrict__ m_p, int *__restrict__ flags) {
+    const int64_t m = *m_p;
+    int f = 0;
+    HDB_GRID_STRIDE(i, m - 1) {
+        double a = cw[i], b = cw[i + 1];
+        if (a < b) f |= 1;
+        if (a > b) f |= 2;
+    }
+    // one atomic per wave (a descending list sets bit 1 in every lane)
+    const uint64_t b1 = __ballot(f & 1), b2 = __ballot(f & 2);
+    f = (b1 ? 1 : 0) | (b2 ? 2 : 0);
+    if ((threadIdx.x & 63) == 0 && f) atomicOr(flags, f);
+}
+
+// rank order by ascending weight: src position of rank r = desc ? m-1-r : (perm ? perm[r] : r)
+__global__ void fl_rank(const int32_t *__restrict__ ca, const int32_t *__restrict__ cb, const double *__restrict__ cw,
+                        int64_t m, int desc, const int32_t *__restrict__ perm, int32_t *__restrict__ ea,
+                        int32_t *__restrict__ eb, double *__restrict__ ew, int32_t *__restrict__ lab,
+                        int32_t *__restrict__ parent) {
+    HDB_GRID_STRIDE(r, m) {
+        int64_t s = desc ? m - 1 - r : (perm ? perm[r] : r);
+        int32_t a = ca[s], b = cb[s];
+        ea[r] = a;
+        eb[r] = b;
+        ew[r] = cw[s];
+        lab[2 * r] = a;  // singleton labels: the vertex id
+        lab[2 * r + 1] = b;
+        parent[r] = NONE;
+    }
+}
+
+__global__ void fl_sort_keys(const double *__restrict__ cw, int64_t m, double *__restrict__ keys,
+                             int32_t *__restrict__ iota) {
+    HDB_GRID_STRIDE(i, m) {
+        keys[i] = cw[i];
+        iota[i] = (int32_t)i;
+    }
+}
+
+__global__ void fill_i32(int32_t *__restrict__ p, int64_t count, int32_t v) {
+    HDB_GRID_STRIDE(i, count) p[i] = v;
+}
+
+// point parents: the lightest edge at each vertex (the dendrogram node a point first joins)
+__global__ void fl_point_parent(const int32_t *__restrict__ ea, const int32_t *__restrict__ eb, int64_t m,
+                                int32_t *__restrict__ pparent) {
+    HDB_GRID_STRIDE(r, m) {
+        atomicMin(&pparent[ea[r]], (int32_t)r);
+        atomicMin(&pparent[eb[r]], (int32_t)r);
+    }
+}
+
+// ------------------------------------------------------- 2. Kruskal tree, depth kernels
+// L edge #i of depth bit b: rank with bit b clear
+__device__ __forceinline__ int64_t l_rank(int64_t i, int b) {
+    return ((i >> b) << (b + 1)) | (i & ((int64_t(1) << b) - 1));
+}
+
+struct DC {
+    int32_t *lab;       // 2m endpoint labels (vertex id < n, or n + root edge rank)
+    int32_t *uf;        // n + m
+    int32_t *stamp;     // n + m: 2j = initialised at depth j, 2j+1 = size counted
+    int32_t *rootedge;  // n + m: largest L edge of the component (at its representative)
+    int32_t *csize;     // n + m
+    int32_t *cmin;      // n + m
+    int32_t *parent;    // m: parent edge rank (NONE: root)
+    int32_t *esize;     // m: |C(e)|
+    int32_t *eminid;    // m: smallest point id in C(e)
+    int64_t n, m;
+};
+
+__global__ void dc_init(DC c, int b, int j, int64_t nl) {
+    HDB_GRID_STRIDE(i, nl) {
+        int64_t r = l_rank(i, b);
+        if (r >= c.m) continue;
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            int32_t x = c.lab[2 * r + s];
+            c.uf[x] = x;
+            c.stamp[x] = 2 * j;
+            c.rootedge[x] = -1;
+            c.csize[x] = 0;
+            c.cmin[x] = NONE;
+        }
+    }
+}
+
+__global__ void dc_unite(DC c, int b, int64_t nl, int *__restrict__ err) {
+    HDB_GRID_STRIDE(i, nl) {
+        int64_t r = l_rank(i, b);
+        if (r >= c.m) continue;
+        if (!uf_unite(c.uf, c.lab[2 * r], c.lab[2 * r + 1])) atomicOr(err, FE_CYCLE);
+    }
+}
+
+// wave reductions (all 64 lanes call them)
+__device__ __forceinline__ int32_t wave_max(int32_t v) {
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int32_t wave_min(int32_t v) {
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int32_t wave_sum(int32_t v) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Shallow depths put most L edges of a wave into one giant component: lanes sharing the
+// first active lane's representative combine (max root edge, summed sizes, min id) and one
+// lane issues the atomics; the others issue their own (same-address atomics serialise).
+__global__ void dc_root(DC c, int b, int j, int64_t nl) {
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < nl; base += stride) {
+        const int64_t i = base + lane;
+        const int64_t r = i < nl ? l_rank(i, b) : c.m;
+        const bool act = r < c.m;
+        const int32_t rep = act ? uf_find(c.uf, c.lab[2 * r]) : -1;
+        const uint64_t am = __ballot(act);
+        if (am == 0) continue;
+        const int leader = __ffsll((unsigned long long)am) - 1;
+        const int32_t rep0 = __shfl(rep, leader);
+        const bool same = act && rep == rep0;
+        int32_t sz = 0, mi = NONE;
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            if (!act) break;
+            int32_t x = c.lab[2 * r + s];
+            // first to count label x (plain read first: a shared label is claimed once)
+            if (((volatile int32_t *)c.stamp)[x] == 2 * j && atomicCAS(&c.stamp[x], 2 * j, 2 * j + 1) == 2 * j) {
+                sz += x < c.n ? 1 : c.esize[x - c.n];
+                mi = min(mi, x < c.n ? x : c.eminid[x - c.n]);
+            }
+        }
+        const int32_t rmax = wave_max(same ? (int32_t)r : -1);
+        const int32_t ssum = wave_sum(same ? sz : 0);
+        const int32_t mmin = wave_min(same ? mi : NONE);
+        if (lane == leader) {
+            atomicMax(&c.rootedge[rep0], rmax);
+            if (ssum) atomicAdd(&c.csize[rep0], ssum);
+            if (mmin != NONE) atomicMin(&c.cmin[rep0], mmin);
+        }
+        if (act && !same) {
+            atomicMax(&c.rootedge[rep], (int32_t)r);
+            if (sz) atomicAdd(&c.csize[rep], sz);
+            if (mi != NONE) atomicMin(&c.cmin[rep], mi);
+        }
+    }
+}
+
+__global__ void dc_link(DC c, int b, int j, int64_t nl) {
+    HDB_GRID_STRIDE(i, nl) {
+        int64_t r = l_rank(i, b);
+        if (r >= c.m) continue;
+        {  // L edge: a component root records |C(e)| and its smallest id
+            const int32_t rep = uf_find(c.uf, c.lab[2 * r]);
+            if (c.rootedge[rep] == (int32_t)r) {
+                c.esize[r] = c.csize[rep];
+                c.eminid[r] = c.cmin[rep];
+            }
+        }
+        const int64_t u = r | (int64_t(1) << b);  // the U edge paired with this thread
+        if (u >= c.m) continue;
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            int32_t x = c.lab[2 * u + s];
+            if (c.stamp[x] == 2 * j + 1) {  // x lies in an L component of this block
+                const int32_t R = c.rootedge[uf_find(c.uf, x)];
+                atomicMin(&c.parent[R], (int32_t)u);
+                c.lab[2 * u + s] = (int32_t)(c.n + R);
+            }
+        }
+    }
+}
+
+// -------------------------------------------------------------------- 3. nodes + clusters
+__global__ void fl_tie_up(const int32_t *__restrict__ parent, const double *__restrict__ ew, int64_t m,
+                          int32_t *__restrict__ up, int *__restrict__ err) {
+    int e = 0;
+    HDB_GRID_STRIDE(r, m) {
+        int32_t p = parent[r];
+        up[r] = (p != NONE && ew[p] == ew[r]) ? p : (int32_t)r;
+        if (p == NONE && r != m - 1) e |= FE_ROOTS;
+    }
+    if (e) atomicOr(err, e);
+}
+
+// synchronous-ish pointer jumping over an upward forest (pointers only move to ancestors, so
+// in-place jumps are safe); flags[k] records whether round k changed anything and round k+1
+// exits at once when it did not.  ~log2(longest chain) rounds do work.
+__global__ void fl_jump(int32_t *__restrict__ up, int64_t m, const int *__restrict__ flag_prev,
+                        int *__restrict__ flag_next) {
+    if (flag_prev && *flag_prev == 0) return;
+    int ch = 0;
+    HDB_GRID_STRIDE(r, m) {
+        int32_t p = up[r];
+        int32_t g = up[p];
+        if (g != p) {
+            int32_t h = up[g];  // two hops per round
+            up[r] = h;
+            ch = 1;
+        }
+    }
+    if (__ballot(ch) && (threadIdx.x & 63) == 0) atomicOr(flag_next, 1);
+}
+
+struct NodeArr {
+    const int32_t *parent, *top, *esize;
+    int32_t *pnode;   // parent node (NONE at the root); only at node ids
+    int32_t *nvalid;  // valid (>= mcs) child nodes
+    int32_t *vsum;    // their total size
+    int64_t m;
+    int32_t mcs;
+};
+
+__global__ void fl_nodes(NodeArr a) {
+    HDB_GRID_STRIDE(r, a.m) {
+        if (a.top[r] != (int32_t)r) continue;  // not a node (merged into a heavier tie edge)
+        int32_t p = a.parent[r];
+        int32_t P = p == NONE ? NONE : a.top[p];
+        a.pnode[r] = P;
+        if (P != NONE && a.esize[r] >= a.mcs) {
+            atomicAdd(&a.nvalid[P], 1);
+            atomicAdd(&a.vsum[P], a.esize[r]);
+        }
+    }
+}
+
+// cluster starts: the root, and each valid child of a node with >= 2 valid children
+__global__ void fl_starts(const int32_t *__restrict__ top, const int32_t *__restrict__ pnode,
+                          const int32_t *__restrict__ esize, const int32_t *__restrict__ nvalid, int64_t m, int32_t mcs,
+                          int32_t *__restrict__ is_start, int32_t *__restrict__ cup) {
+    HDB_GRID_STRIDE(r, m) {
+        int32_t s = 0, u = (int32_t)r;
+        if (top[r] == (int32_t)r) {
+            int32_t P = pnode[r];
+            s = (P == NONE) || (esize[r] >= mcs && nvalid[P] >= 2);
+            u = s ? (int32_t)r : P;
+        }
+        is_start[r] = s;
+        cup[r] = u;
+    }
+}
+
+// stability terms of the reached nodes outside the root cluster, keyed (cluster, -rank)
+__global__ void fl_terms(const int32_t *__restrict__ top, const int32_t *__restrict__ pnode,
+                         const int32_t *__restrict__ cs, const int32_t *__restrict__ cid,
+                         const int32_t *__restrict__ esize, const int32_t *__restrict__ nvalid,
+                         const int32_t *__restrict__ vsum, const double *__restrict__ ew, int64_t m, int32_t mcs,
+                         uint64_t *__restrict__ key, double *__restrict__ val) {
+    HDB_GRID_STRIDE(r, m) {
+        uint64_t k = ~uint64_t(0);
+        double v = 0.0;
+        const int32_t root = (int32_t)(m - 1);
+        if (top[r] == (int32_t)r && esize[r] >= mcs) {  // reached (the root cluster is skipped)
+            const int32_t L = cs[r];
+            if (L != root) {
+                const double eps = ew[r];
+                const double inv_birth = 1.0 / ew[pnode[L]];
+                const int32_t nv = nvalid[r];
+                int64_t pts = nv == 1 ? (int64_t)esize[r] - vsum[r] : esize[r];
+                if (pts > 0) {
+                    v = (double)pts * (1.0 / eps - inv_birth);  // Cluster.detachPoints
+                    k = ((uint64_t)(uint32_t)cid[L] << 32) | (uint32_t)(m - 1 - r);
+                }
+            }
+        }
+        key[r] = k;
+        val[r] = v;
+    }
+}
+
+// one wave per cluster: lanes stage the chain's terms through LDS (coalesced, the next chunk
+// in flight), lane 0 adds them in order -- the host's sequential sum, descending level
+constexpr int STAB_CHUNK = 256;
+__global__ __launch_bounds__(64) void fl_stab(const double *__restrict__ val, const int32_t *__restrict__ seg_lo,
+                                              const int32_t *__restrict__ seg_hi, int32_t nc,
+                                              double *__restrict__ stab) {
+    __shared__ double buf[STAB_CHUNK];
+    const int lane = threadIdx.x;
+    for (int32_t c = blockIdx.x; c < nc; c += gridDim.x) {
+        const int64_t lo = seg_lo[c], hi = lo < 0 ? -1 : seg_hi[c];
+        double s = 0.0;
+        double nxt[STAB_CHUNK / 64];
+        auto load = [&](int64_t base) {
+#pragma unroll
+            for (int k = 0; k < STAB_CHUNK / 64; k++) {
+                int64_t i = base + k * 64 + lane;
+                nxt[k] = i < hi ? val[i] : 0.0;
+            }
+        };
+        if (lo >= 0) load(lo);
+        for (int64_t base = lo; lo >= 0 && base < hi; base += STAB_CHUNK) {
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < STAB_CHUNK / 64; k++) buf[k * 64 + lane] = nxt[k];
+            __syncthreads();
+            if (base + STAB_CHUNK < hi) load(base + STAB_CHUNK);  // overlaps lane 0's adds
+            if (lane == 0) {
+                const int cnt = hi - base < STAB_CHUNK ? (int)(hi - base) : STAB_CHUNK;
+                for (int k = 0; k < cnt; k++) s = s + buf[k];
+            }
+        }
+        if (lane == 0) stab[c] = s;
+    }
+}
+
+__global__ void fl_seg(const uint64_t *__restrict__ key, int64_t m, int32_t *__restrict__ seg_lo,
+                       int32_t *__restrict__ seg_hi) {
+    HDB_GRID_STRIDE(i, m) {
+        uint64_t k = key[i];
+        if (k == ~uint64_t(0)) continue;
+        int32_t c = (int32_t)(k >> 32);
+        if (i == 0 || (int32_t)(key[i - 1] >> 32) != c) seg_lo[c] = (int32_t)i;
+        if (i == m - 1 || (int32_t)(key[i + 1] >> 32) != c) seg_hi[c] = (int32_t)(i + 1);
+    }
+}
+
+__global__ void fl_cluster_meta(const int32_t *__restrict__ is_start, const int32_t *__restrict__ cid,
+                                const int32_t *__restrict__ cs, const int32_t *__restrict__ pnode,
+                                const int32_t *__restrict__ eminid, int64_t m, int32_t *__restrict__ cpar,
+                                int32_t *__restrict__ cmin) {
+    HDB_GRID_STRIDE(r, m) {
+        if (!is_start[r]) continue;
+        int32_t c = cid[r];
+        int32_t P = pnode[r];
+        cpar[c] = P == NONE ? -1 : cid[cs[P]];
+        cmin[c] = eminid[r];
+    }
+}
+
+// labels: a point's node -> its cluster (cs) -> the label of the nearest selected ancestor
+// cluster (propagated over the cluster tree on the host; 0 = none)
+__global__ void fl_point_labels(const int32_t *__restrict__ pparent, const int32_t *__restrict__ top,
+                                const int32_t *__restrict__ cs, const int32_t *__restrict__ cid,
+                                const int32_t *__restrict__ clab, int64_t n, int32_t *__restrict__ labels) {
+    HDB_GRID_STRIDE(v, n) labels[v] = clab[cid[cs[top[pparent[v]]]]];
+}
+
+inline int grid_for(int64_t count) { return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(count, 256), 16384)); }
+
+struct Carver {
+    char *base = nullptr;
+    size_t off = 0;
+    template <class T>
+    T *take(int64_t count) {
+        size_t o = off;
+        off += ((size_t)std::max<int64_t>(count, 1) * sizeof(T) + 255) & ~size_t(255);
+        return base ? (T *)(base + o) : nullptr;
+    }
+};
+
+}  // namespace
+
+void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, const double *w, int64_t ne, int64_t n,
+                        int32_t mcs, int32_t *labels, int64_t *n_clusters) {
+    if (n <= 0) {
+        if (n_clusters) *n_clusters = 0;
+        return;
+    }
+    if (mcs < 2) HDB_THROW(HDB_EINVAL, "flat labels: minClSize must be >= 2");
+    if (n >= (int64_t(1) << 30)) HDB_THROW(HDB_EINVAL, "flat labels: too many points");
+    if (ne < 0) HDB_THROW(HDB_EINVAL, "bad arguments");
+    hipStream_t st = ctx->stream;
+    KernelTimer tt(ctx, "flat_labels");
+    const int64_t m = n - 1;  // a spanning tree has exactly n - 1 non-self edges
+    int64_t *pin = pinned_words(ctx) + PINNED_WORDS - 8;  // private slice
+    const int64_t mm = std::max<int64_t>(m, 1);
+
+    // scratch: sizes are fixed by n and ne
+    auto layout = [&](Carver &cv) {
+        cv.take<int32_t>(ne);            // keep
+        cv.take<int32_t>(ne);            // pos
+        cv.take<int32_t>(mm);            // ca
+        cv.take<int32_t>(mm);            // cb
+        cv.take<double>(mm);             // cw
+        cv.take<int64_t>(4);             // m_dev, err, flags
+        cv.take<int32_t>(mm);            // ea
+        cv.take<int32_t>(mm);            // eb
+        cv.take<double>(mm);             // ew
+        cv.take<int32_t>(2 * mm);        // lab
+        for (int k = 0; k < 5; k++) cv.take<int32_t>(n + mm);  // uf stamp rootedge csize cmin
+        for (int k = 0; k < 3; k++) cv.take<int32_t>(mm);      // parent esize eminid
+        cv.take<int32_t>(n);             // pparent
+    };
+    Carver probe;
+    layout(probe);
+    Carver cv{(char *)arena(ctx, A_FLAT0, probe.off), 0};
+    int32_t *keep = cv.take<int32_t>(ne), *pos = cv.take<int32_t>(ne);
+    int32_t *ca = cv.take<int32_t>(mm), *cb = cv.take<int32_t>(mm);
+    double *cw = cv.take<double>(mm);
+    int64_t *words = cv.take<int64_t>(4);
+    int64_t *m_dev = words;
+    int *err = (int *)(words + 1), *flags = (int *)(words + 2);
+    int32_t *ea = cv.take<int32_t>(mm), *eb = cv.take<int32_t>(mm);
+    double *ew = cv.take<double>(mm);
+    DC dc;
+    dc.lab = cv.take<int32_t>(2 * mm);
+    dc.uf = cv.take<int32_t>(n + mm);
+    dc.stamp = cv.take<int32_t>(n + mm);
+    dc.rootedge = cv.take<int32_t>(n + mm);
+    dc.csize = cv.take<int32_t>(n + mm);
+    dc.cmin = cv.take<int32_t>(n + mm);
+    dc.parent = cv.take<int32_t>(mm);
+    dc.esize = cv.take<int32_t>(mm);
+    dc.eminid = cv.take<int32_t>(mm);
+    int32_t *pparent = cv.take<int32_t>(n);
+    dc.n = n;
+    dc.m = m;
+
+    HIP_CHECK(hipMemsetAsync(words, 0, sizeof(int64_t) * 4, st));
+    // ---- 1. compact, validate, order
+    if (ne > 0) {
+        if (ne > INT32_MAX) HDB_THROW(HDB_EINVAL, "too many edges");
+        hipLaunchKernelGGL(fl_mark, dim3(grid_for(ne)), dim3(256), 0, st, va, vb, w, ne, n, keep, err);
+        size_t tb = 0;
+        HIP_CHECK(rocprim::exclusive_scan(nullptr, tb, keep, pos, 0, (size_t)ne, rocprim::plus<int32_t>(), st));
+        void *tmp = arena(ctx, A_FLAT_TMP, tb);
+        HIP_CHECK(rocprim::exclusive_scan(tmp, tb, keep, pos, 0, (size_t)ne, rocprim::plus<int32_t>(), st));
+        hipLaunchKernelGGL(fl_compact, dim3(grid_for(ne)), dim3(256), 0, st, va, vb, w, ne, keep, pos, m, ca, cb, cw,
+                           m_dev);
+        hipLaunchKernelGGL(fl_order, dim3(grid_for(ne)), dim3(256), 0, st, cw, m_dev, flags);
+    }
+    HIP_CHECK(hipMemcpyAsync(pin, words, sizeof(int64_t) * 3, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    const int64_t m_got = pin[0];
+    const int e0 = (int)pin[1], order = (int)pin[2];
+    if (e0 & FE_RANGE) HDB_THROW(HDB_EINVAL, "flat labels: vertex id out of range");
+    if (e0 & FE_NAN) HDB_THROW(HDB_EINVAL, "flat labels: NaN edge weight");
+    if (m_got != m) HDB_THROW(HDB_EINVAL, "flat labels: the edges are not a spanning tree");
+    if (m == 0) {  // one point: no hierarchy below the root
+        HIP_CHECK(hipMemsetAsync(labels, 0, sizeof(int32_t), st));
+        if (n_clusters) *n_clusters = 0;
+        return;
+    }
+    const int g = grid_for(m);
+    const int32_t *perm = nullptr;
+    int desc = !(order & 1);
+    if (desc == 0 && (order & 2)) {  // neither ascending nor descending: radix sort by weight
+        Carver sp;
+        sp.take<double>(m);
+        sp.take<double>(m);
+        sp.take<int32_t>(m);
+        sp.take<int32_t>(m);
+        Carver sc{(char *)arena(ctx, A_FLAT1, sp.off), 0};
+        double *k1 = sc.take<double>(m), *k2 = sc.take<double>(m);
+        int32_t *i1 = sc.take<int32_t>(m), *i2 = sc.take<int32_t>(m);
+        hipLaunchKernelGGL(fl_sort_keys, dim3(g), dim3(256), 0, st, cw, m, k1, i1);
+        size_t tb = 0;
+        HIP_CHECK(sort_pairs(nullptr, tb, k1, k2, i1, i2, m, 0, 64, st));
+        void *tmp = arena(ctx, A_FLAT_TMP, tb);
+        HIP_CHECK(sort_pairs(tmp, tb, k1, k2, i1, i2, m, 0, 64, st));
+        perm = i2;
+    }
+    hipLaunchKernelGGL(fl_rank, dim3(g), dim3(256), 0, st, ca, cb, cw, m, desc, perm, ea, eb, ew, dc.lab, dc.parent);
+    hipLaunchKernelGGL(fill_i32, dim3(grid_for(n + m)), dim3(256), 0, st, dc.stamp, n + m, -1);
+    hipLaunchKernelGGL(fill_i32, dim3(grid_for(n)), dim3(256), 0, st, pparent, n, NONE);
+    hipLaunchKernelGGL(fl_point_parent, dim3(g), dim3(256), 0, st, ea, eb, m, pparent);
+
+    // ---- 2. Kruskal tree by rank divide and conquer
+    int J = 0;
+    while ((int64_t(1) << J) <= m) J++;  // 2^J > m: every rank < m has a clear bit below J
+    for (int j = 0; j < J; j++) {
+        const int b = J - 1 - j;
+        // L ranks (bit b clear) below m; every U rank is an L rank + 2^b
+        const int64_t blk = int64_t(1) << (b + 1), half = int64_t(1) << b;
+        const int64_t nl = (m / blk) * half + std::min(m % blk, half);
+        const int gl = grid_for(nl);
+        hipLaunchKernelGGL(dc_init, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
+        hipLaunchKernelGGL(dc_unite, dim3(gl), dim3(256), 0, st, dc, b, nl, err);
+        hipLaunchKernelGGL(dc_root, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
+        hipLaunchKernelGGL(dc_link, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
+    }
+
+    // ---- 3. multi-way nodes, condensation
+    // reuse the union-find scratch (n + m ints each) for the node arrays
+    int32_t *top = dc.uf, *pnode = dc.stamp, *nvalid = dc.rootedge, *vsum = dc.csize, *is_start = dc.cmin;
+    Carver nc2{nullptr, 0};
+    nc2.take<int32_t>(m);  // cup / cs
+    nc2.take<int32_t>(m);  // cid
+    nc2.take<uint64_t>(m);
+    nc2.take<uint64_t>(m);
+    nc2.take<double>(m);
+    nc2.take<double>(m);
+    nc2.take<int32_t>(m);  // seg
+    nc2.take<double>(m);   // stab
+    nc2.take<int32_t>(m);  // cpar
+    nc2.take<int32_t>(m);  // cminid
+    nc2.take<int32_t>(m);  // clab
+    nc2.take<int32_t>(64);  // jump flags
+    nc2.take<int64_t>(1);  // cluster count
+    Carver cv2{(char *)arena(ctx, A_FLAT1, nc2.off), 0};
+    int32_t *cs = cv2.take<int32_t>(m), *cid = cv2.take<int32_t>(m);
+    uint64_t *key1 = cv2.take<uint64_t>(m), *key2 = cv2.take<uint64_t>(m);
+    double *val1 = cv2.take<double>(m), *val2 = cv2.take<double>(m);
+    int32_t *seg = cv2.take<int32_t>(m);
+    double *stab = cv2.take<double>(m);
+    int32_t *cpar = cv2.take<int32_t>(m), *cminid = cv2.take<int32_t>(m), *clab = cv2.take<int32_t>(m);
+    int *jflags = cv2.take<int32_t>(64);
+    int rounds = 2;
+    for (int64_t span = 3; span < m; span *= 3) rounds++;
+    rounds = std::min(rounds, 64);
+    auto jump_all = [&](int32_t *up) {  // roots of an upward forest, in place
+        HIP_CHECK(hipMemsetAsync(jflags, 0, sizeof(int) * 64, st));
+        for (int k = 0; k < rounds; k++)
+            hipLaunchKernelGGL(fl_jump, dim3(g), dim3(256), 0, st, up, m, k ? jflags + k - 1 : nullptr, jflags + k);
+    };
+
+    hipLaunchKernelGGL(fl_tie_up, dim3(g), dim3(256), 0, st, dc.parent, ew, m, top, err);
+    jump_all(top);
+    HIP_CHECK(hipMemsetAsync(nvalid, 0, sizeof(int32_t) * m, st));
+    HIP_CHECK(hipMemsetAsync(vsum, 0, sizeof(int32_t) * m, st));
+    NodeArr na{dc.parent, top, dc.esize, pnode, nvalid, vsum, m, mcs};
+    hipLaunchKernelGGL(fl_nodes, dim3(g), dim3(256), 0, st, na);
+    hipLaunchKernelGGL(fl_starts, dim3(g), dim3(256), 0, st, top, pnode, dc.esize, nvalid, m, mcs, is_start, cs);
+    jump_all(cs);
+    {
+        size_t tb = 0;
+        HIP_CHECK(rocprim::exclusive_scan(nullptr, tb, is_start, cid, 0, (size_t)m, rocprim::plus<int32_t>(), st));
+        void *tmp = arena(ctx, A_FLAT_TMP, tb);
+        HIP_CHECK(rocprim::exclusive_scan(tmp, tb, is_start, cid, 0, (size_t)m, rocprim::plus<int32_t>(), st));
+    }
+    // the root (rank m-1) always starts a cluster: count = cid[m-1] + 1
+    HIP_CHECK(hipMemcpyAsync(pin, cid + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(pin + 1, err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    const int e1 = *(int *)(pin + 1);
+    if (e1 & FE_CYCLE) HDB_THROW(HDB_EINVAL, "flat labels: the edges contain a cycle");
+    if (e1 & FE_ROOTS) HDB_THROW(HDB_EINVAL, "flat labels: the edges are not a spanning tree");
+    const int32_t K = *(int32_t *)pin + 1;  // clusters incl. the root (cid K-1)
+
+    // ---- 4. stabilities: chains grouped by cluster, descending level inside
+    hipLaunchKernelGGL(fl_terms, dim3(g), dim3(256), 0, st, top, pnode, cs, cid, dc.esize, nvalid, vsum, ew, m, mcs,
+                       key1, val1);
+    int kb = 0;
+    while ((int64_t(1) << kb) < (int64_t)K + 1) kb++;
+    {
+        size_t tb = 0;
+        // keys of non-terms are all-ones: sorting on the cluster bits + 32 keeps them last
+        HIP_CHECK(sort_pairs(nullptr, tb, key1, key2, val1, val2, m, 0, 64, st));
+        void *tmp = arena(ctx, A_FLAT_TMP, tb);
+        HIP_CHECK(sort_pairs(tmp, tb, key1, key2, val1, val2, m, 0, std::min(64, 32 + kb + 1), st));
+    }
+    int32_t *seg_hi = (int32_t *)key1;  // key1 is free after the sort
+    hipLaunchKernelGGL(fill_i32, dim3(grid_for(K)), dim3(256), 0, st, seg, K, -1);
+    hipLaunchKernelGGL(fl_seg, dim3(g), dim3(256), 0, st, key2, m, seg, seg_hi);
+    hipLaunchKernelGGL(fl_stab, dim3((int)std::min<int64_t>(K, 65536)), dim3(64), 0, st, val2, seg, seg_hi, K, stab);
+    hipLaunchKernelGGL(fl_cluster_meta, dim3(g), dim3(256), 0, st, is_start, cid, cs, pnode, dc.eminid, m, cpar, cminid);
+    std::vector<int32_t> hpar(K), hmin(K), hlab(K, 0);
+    std::vector<double> hstab(K);
+    HIP_CHECK(hipMemcpyAsync(hpar.data(), cpar, sizeof(int32_t) * K, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(hmin.data(), cminid, sizeof(int32_t) * K, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(hstab.data(), stab, sizeof(double) * K, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+
+    // FOSC (flat.cpp step 3) over the K clusters: ids ascend with the start node's rank, so a
+    // child cluster always precedes its parent; the root is K-1
+    std::vector<int32_t> koff(K + 1, 0), kids(K);
+    for (int32_t c = 0; c < K - 1; c++) koff[hpar[c] + 1]++;
+    for (int32_t c = 0; c < K; c++) koff[c + 1] += koff[c];
+    {
+        std::vector<int32_t> fill(koff.begin(), koff.end() - 1);
+        for (int32_t c = 0; c < K - 1; c++) kids[fill[hpar[c]]++] = c;
+    }
+    for (int32_t c = 0; c < K; c++)
+        std::sort(kids.begin() + koff[c], kids.begin() + koff[c + 1],
+                  [&](int32_t a, int32_t b) { return hmin[a] < hmin[b]; });
+    std::vector<double> contrib(K, 0.0);
+    std::vector<char> self_sel(K, 0);
+    for (int32_t c = 0; c < K - 1; c++) {
+        double prop = 0.0;
+        for (int32_t k = koff[c]; k < koff[c + 1]; k++) prop = prop + contrib[kids[k]];
+        if (koff[c + 1] == koff[c] || hstab[c] >= prop) {  // Cluster.propagate: ties keep the parent
+            contrib[c] = hstab[c];
+            self_sel[c] = 1;
+        } else {
+            contrib[c] = prop;
+        }
+    }
+    std::vector<int32_t> sel, todo(kids.begin() + koff[K - 1], kids.begin() + koff[K]);
+    while (!todo.empty()) {
+        int32_t c = todo.back();
+        todo.pop_back();
+        if (self_sel[c]) sel.push_back(c);
+        else todo.insert(todo.end(), kids.begin() + koff[c], kids.begin() + koff[c + 1]);
+    }
+    std::sort(sel.begin(), sel.end(), [&](int32_t a, int32_t b) { return hmin[a] < hmin[b]; });
+    for (size_t i = 0; i < sel.size(); i++) hlab[sel[i]] = (int32_t)(i + 1);
+    // every cluster takes the label of its nearest selected ancestor-or-self (parents have
+    // larger ids: top-down is descending id); the root keeps 0
+    for (int32_t c = K - 2; c >= 0; c--)
+        if (hlab[c] == 0) hlab[c] = hlab[hpar[c]];    HIP_CHECK(hipMemcpyAsync(clab, hlab.data(), sizeof(int32_t) * K, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(fl_point_labels, dim3(grid_for(n)), dim3(256), 0, st, pparent, top, cs, cid, clab, n,
+                       labels);
+    HIP_CHECK(hipGetLastError());
+    // hlab is read by the queued copy: wait before it goes out of scope
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (n_clusters) *n_clusters = (int64_t)sel.size();
+}
+
+}  // namespace hdb

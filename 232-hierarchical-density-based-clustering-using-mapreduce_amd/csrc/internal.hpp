@@ -51,6 +51,10 @@ void exact_leaf_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int min_
 void boruvka_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const double *core, int metric, int32_t *va,
                     int32_t *vb, double *w);
 
+// K6: global hierarchy + flat labels over a merged MST (flat.hip); synchronises
+void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, const double *w, int64_t ne, int64_t n,
+                        int32_t mcs, int32_t *labels, int64_t *n_clusters);
+
 // host logic (local_model.cpp)
 int bubble_core_epilogue(const double *rep, const int32_t *nB, const double *eB, const double *nnB, int64_t b, int d,
                          int min_pts, int metric, const double *knn, const int32_t *log, double *core);

@@ -213,12 +213,13 @@ def flat_labels(va, vb, w, n: int, minClSize: int, ctx=None):
     """Global HDBSCAN* flat partition over a merged MST (the reference's
     Main.java:351-408 never completes it): HDBSCANStar.java:208-625 semantics, canonical tie
     rules.  Returns (labels[n] with 1..K by smallest member id and 0 = noise, K).
-    Host arrays run the host algorithm without a device; device tensors are staged once."""
+    Device tensors, or any arrays with a ctx, run the device algorithm (K6, csrc/flat.hip);
+    host arrays without a ctx run the host algorithm (csrc/flat.cpp) with no device."""
     a, b, ww = A.Arr(va, np.int32), A.Arr(vb, np.int32), A.Arr(w, np.float64)
     labels = A.new_like(a, (n,), np.int32)
     k = np.zeros(1, np.int64)
     on_dev = a.device is not None and a.device.type == "cuda"
-    h = (ctx or A.Context.get(a.device.index or 0)).h if on_dev else None
+    h = ctx.h if ctx is not None else (A.Context.get(a.device.index or 0).h if on_dev else None)
     A.check(A.lib().hdb_flat_labels(h, a.p, b.p, ww.p, ww.obj.shape[0], n, minClSize, A.ptr(labels), A.ptr(k)),
             "flat_labels")
     return labels, int(k[0])

@@ -2,6 +2,9 @@
 the line restatement of Main.java:103-347 with the deviations D1-D10) on ALL 245,057 rows of
 the reference's Skin_NonSkin.txt with the reference's hard-coded my_args (Main.java:71:
 minPts=4, minClSize=4, processing_units=50, k=0.2) and the D2 sample seed 20210101.
+Level 0's bubble model (49,012 bubbles) raises the reference's own exception
+(Clusters.java:45-46, HDB_EREF_NEGATIVE_CLUSTER); D10 records it and the subset becomes one
+forced leaf, so the whole file runs the exact leaf MST (~20 min of oracle Prim).
 
 Run in the build container (the oracle is test infrastructure; takes minutes):
     python tests/golden/make_c1.py
@@ -31,6 +34,7 @@ def main(out=os.path.join(HERE, "c1_skin_full.npz")):
     va, vb, w = r["edges"]
     lv = []  # per level: (iteration, key, kind, count) rows; kind 0 leaf, 1 big
     lab_keys, lab_off, lab_vals, nk_keys, nk_off, nk_vals = [], [0], [], [], [0], []
+    errs = []  # D10: (iteration, key, code) of local models that raise the reference's exception
     for L in r["levels"]:
         for k, c in sorted(L["leaves"].items()):
             lv.append((L["iteration"], k, 0, c))
@@ -44,7 +48,8 @@ def main(out=os.path.join(HERE, "c1_skin_full.npz")):
             nk_keys.append((L["iteration"], k))
             nk_vals.append(np.asarray(L["new_keys"][k], np.int64))
             nk_off.append(nk_off[-1] + len(L["new_keys"][k]))
-        assert not L.get("model_errors"), L.get("model_errors")
+        for k, code in sorted(L.get("model_errors", {}).items()):
+            errs.append((L["iteration"], k, code))
     cat = lambda a, t: np.concatenate(a).astype(t) if a else np.zeros(0, t)
     np.savez_compressed(
         out, va=va, vb=vb, w=w, leaf_of=r["leaf_of"], labels=r["labels"], n_clusters=r["n_clusters"],
@@ -52,6 +57,7 @@ def main(out=os.path.join(HERE, "c1_skin_full.npz")):
         label_keys=np.asarray(lab_keys, np.int64).reshape(-1, 2), label_off=np.asarray(lab_off, np.int64),
         label_vals=cat(lab_vals, np.int32), newkey_keys=np.asarray(nk_keys, np.int64).reshape(-1, 2),
         newkey_off=np.asarray(nk_off, np.int64), newkey_vals=cat(nk_vals, np.int64),
+        model_errors=np.asarray(errs, np.int64).reshape(-1, 3),
         args=np.asarray([ARGS["min_pts"], ARGS["min_cl_size"], ARGS["processing_units"], ARGS["seed"]], np.int64),
         k=ARGS["k"])
     print("wrote", out, os.path.getsize(out), "bytes")

@@ -4,9 +4,9 @@ ALL 245,057 rows of the reference's Skin_NonSkin.txt with the reference's hard-c
 
 The expected outputs are the CPU oracle's (oracle/mr_driver.py over hdb_oracle.c, the line
 restatement of Main.java:103-347 with the deviations D1-D10), committed as
-tests/golden/c1_skin_full.npz by tests/golden/make_c1.py.  Level 0 samples 49,012 points,
-the bubble model yields a single label, so D9 turns the whole file into one
-forced leaf: the leaf runs the reference Prim on 245,057 points (exact_prim_leaves), and the
+tests/golden/c1_skin_full.npz by tests/golden/make_c1.py.  Level 0 samples 49,012 points;
+the bubble model raises the reference's own Clusters.java:45-46 exception on them (D10 records
+it, HDB_EREF_NEGATIVE_CLUSTER), so the whole file becomes one forced leaf: the leaf runs the reference Prim on 245,057 points (exact_prim_leaves), and the
 edge list must equal the oracle's bit for bit, ties included."""
 import time
 
@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _levels(got):
-    lv, labels, new_keys = [], {}, {}
+    lv, labels, new_keys, errs = [], {}, {}, []
     for L in got["levels"]:
         for k, c in sorted(L["leaves"].items()):
             lv.append((L["iteration"], k, 0, c))
@@ -29,13 +29,15 @@ def _levels(got):
             labels[(L["iteration"], k)] = np.asarray(L["labels"][k], np.int32)
         for k in L["new_keys"]:
             new_keys[(L["iteration"], k)] = list(L["new_keys"][k])
-        assert not L.get("model_errors")
-    return np.asarray(lv, np.int64).reshape(-1, 4), labels, new_keys
+        for k, code in sorted(L.get("model_errors", {}).items()):
+            errs.append((L["iteration"], k, code))
+    return np.asarray(lv, np.int64).reshape(-1, 4), labels, new_keys, np.asarray(errs, np.int64).reshape(-1, 3)
 
 
 def _check_structure(G, got):
-    lv, labels, new_keys = _levels(got)
+    lv, labels, new_keys, errs = _levels(got)
     assert got["iterations"] == int(G["iterations"])
+    assert np.array_equal(errs, G["model_errors"])  # D10: the reference's exception, same level
     assert np.array_equal(lv, G["levels"])
     assert len(labels) == G["label_keys"].shape[0]
     for i, (it, k) in enumerate(G["label_keys"].tolist()):
