@@ -42,10 +42,20 @@ namespace {
 constexpr int32_t NONE = INT32_MAX;
 enum : int { FE_RANGE = 1, FE_NAN = 2, FE_CYCLE = 4, FE_ISOLATED = 8, FE_ROOTS = 16 };
 
-// --------------------------------------------------------------- union-find (parent >= id)
-// Roots hook under the LARGER id: a contracted label n + R that many edges share (a giant
-// component of the lower half) stays a root while singleton labels hook under it -- no CAS
-// contention on one entry.
+// ------------------------------------------------------------------------- union-find
+// Randomised linking: the root with the lower (priority, id) hooks under the higher one, so
+// trees stay O(log) deep whatever order the unions arrive in (linking by id alone builds
+// long chains on the ascending-id paths of an MST).  Contracted labels (>= n: a component of
+// the lower ranks, often shared by thousands of edges) outrank every vertex label, so the
+// many unions of singletons with a shared label CAS their own entries, never the shared one.
+__device__ __forceinline__ uint32_t uf_prio(int32_t x, int64_t n) {
+    uint32_t h = (uint32_t)x * 0x9E3779B1u;
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    return (x >= n ? 0x80000000u : 0u) | (h >> 1);
+}
+
 __device__ __forceinline__ int32_t uf_find(int32_t *uf, int32_t x) {
     volatile int32_t *u = uf;
     while (true) {
@@ -58,18 +68,30 @@ __device__ __forceinline__ int32_t uf_find(int32_t *uf, int32_t x) {
     }
 }
 
-__device__ __forceinline__ bool uf_unite(int32_t *uf, int32_t a, int32_t b) {
+__device__ __forceinline__ bool uf_unite(int32_t *uf, int32_t a, int32_t b, int64_t n) {
     while (true) {
         a = uf_find(uf, a);
         b = uf_find(uf, b);
         if (a == b) return false;
-        if (a < b) {
+        const uint32_t pa = uf_prio(a, n), pb = uf_prio(b, n);
+        if (pa < pb || (pa == pb && a < b)) {
             int32_t t = a;
             a = b;
             b = t;
         }
-        if (atomicCAS(&uf[b], b, a) == b) return true;  // b < a
+        if (atomicCAS(&uf[b], b, a) == b) return true;  // b hooks under the higher-priority a
     }
+}
+
+// set bit(s) of a flag word once per workgroup (same-address atomics and even GLC reads
+// from thousands of waves serialise at one L2 channel); every thread must call it
+__device__ __forceinline__ void flag_or(int *flag, int bits) {
+    __shared__ int sbits;
+    if (threadIdx.x == 0) sbits = 0;
+    __syncthreads();
+    if (bits) atomicOr(&sbits, bits);
+    __syncthreads();
+    if (threadIdx.x == 0 && sbits) atomicOr(flag, sbits);
 }
 
 // root of x in an "upward" forest (every pointer goes to a larger id, roots point to self),
@@ -129,10 +151,7 @@ __global__ void fl_order(const double *__restrict__ cw, const int64_t *__restric
         if (a < b) f |= 1;
         if (a > b) f |= 2;
     }
-    // one atomic per wave (a descending list sets bit 1 in every lane)
-    const uint64_t b1 = __ballot(f & 1), b2 = __ballot(f & 2);
-    f = (b1 ? 1 : 0) | (b2 ? 2 : 0);
-    if ((threadIdx.x & 63) == 0 && f) atomicOr(flags, f);
+    flag_or(flags, f);  // a descending list sets bit 1 in every lane
 }
 
 // rank order by ascending weight: src position of rank r = desc ? m-1-r : (perm ? perm[r] : r)
@@ -212,7 +231,7 @@ __global__ void dc_unite(DC c, int b, int64_t nl, int *__restrict__ err) {
     HDB_GRID_STRIDE(i, nl) {
         int64_t r = l_rank(i, b);
         if (r >= c.m) continue;
-        if (!uf_unite(c.uf, c.lab[2 * r], c.lab[2 * r + 1])) atomicOr(err, FE_CYCLE);
+        if (!uf_unite(c.uf, c.lab[2 * r], c.lab[2 * r + 1], c.n)) atomicOr(err, FE_CYCLE);  // rare: bad input
     }
 }
 
@@ -230,46 +249,56 @@ __device__ __forceinline__ int32_t wave_sum(int32_t v) {
     return v;
 }
 
-// Shallow depths put most L edges of a wave into one giant component: lanes sharing the
-// first active lane's representative combine (max root edge, summed sizes, min id) and one
-// lane issues the atomics; the others issue their own (same-address atomics serialise).
-__global__ void dc_root(DC c, int b, int j, int64_t nl) {
-    const int lane = threadIdx.x & 63;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < nl; base += stride) {
-        const int64_t i = base + lane;
+// Per component: largest L edge, summed label sizes, smallest id.  Shallow depths put most L
+// edges into a few giant components, so a workgroup first combines its lanes' contributions
+// in an LDS table keyed by representative (LDS atomics), then issues one global atomic per
+// distinct representative.
+constexpr int ROOT_TB = 256, ROOT_SLOTS = 512;
+__global__ __launch_bounds__(ROOT_TB) void dc_root(DC c, int b, int j, int64_t nl) {
+    __shared__ int32_t skey[ROOT_SLOTS], smax[ROOT_SLOTS], ssum[ROOT_SLOTS], smin[ROOT_SLOTS];
+    const int t = threadIdx.x;
+    for (int64_t base = (int64_t)blockIdx.x * ROOT_TB; base < nl; base += (int64_t)gridDim.x * ROOT_TB) {
+        for (int k = t; k < ROOT_SLOTS; k += ROOT_TB) {
+            skey[k] = -1;
+            smax[k] = -1;
+            ssum[k] = 0;
+            smin[k] = NONE;
+        }
+        __syncthreads();
+        const int64_t i = base + t;
         const int64_t r = i < nl ? l_rank(i, b) : c.m;
-        const bool act = r < c.m;
-        const int32_t rep = act ? uf_find(c.uf, c.lab[2 * r]) : -1;
-        const uint64_t am = __ballot(act);
-        if (am == 0) continue;
-        const int leader = __ffsll((unsigned long long)am) - 1;
-        const int32_t rep0 = __shfl(rep, leader);
-        const bool same = act && rep == rep0;
-        int32_t sz = 0, mi = NONE;
+        if (r < c.m) {
+            const int32_t rep = uf_find(c.uf, c.lab[2 * r]);
+            int32_t sz = 0, mi = NONE;
 #pragma unroll
-        for (int s = 0; s < 2; s++) {
-            if (!act) break;
-            int32_t x = c.lab[2 * r + s];
-            // first to count label x (plain read first: a shared label is claimed once)
-            if (((volatile int32_t *)c.stamp)[x] == 2 * j && atomicCAS(&c.stamp[x], 2 * j, 2 * j + 1) == 2 * j) {
-                sz += x < c.n ? 1 : c.esize[x - c.n];
-                mi = min(mi, x < c.n ? x : c.eminid[x - c.n]);
+            for (int s = 0; s < 2; s++) {
+                int32_t x = c.lab[2 * r + s];
+                // first to count label x (plain read first: a shared label is claimed once)
+                if (((volatile int32_t *)c.stamp)[x] == 2 * j &&
+                    atomicCAS(&c.stamp[x], 2 * j, 2 * j + 1) == 2 * j) {
+                    sz += x < c.n ? 1 : c.esize[x - c.n];
+                    mi = min(mi, x < c.n ? x : c.eminid[x - c.n]);
+                }
             }
+            uint32_t h = uf_prio(rep, 0) & (ROOT_SLOTS - 1);
+            while (true) {  // <= ROOT_TB distinct keys in 2x slots: always finds one
+                int32_t k = atomicCAS(&skey[h], -1, rep);
+                if (k == -1 || k == rep) break;
+                h = (h + 1) & (ROOT_SLOTS - 1);
+            }
+            atomicMax(&smax[h], (int32_t)r);
+            if (sz) atomicAdd(&ssum[h], sz);
+            if (mi != NONE) atomicMin(&smin[h], mi);
         }
-        const int32_t rmax = wave_max(same ? (int32_t)r : -1);
-        const int32_t ssum = wave_sum(same ? sz : 0);
-        const int32_t mmin = wave_min(same ? mi : NONE);
-        if (lane == leader) {
-            atomicMax(&c.rootedge[rep0], rmax);
-            if (ssum) atomicAdd(&c.csize[rep0], ssum);
-            if (mmin != NONE) atomicMin(&c.cmin[rep0], mmin);
+        __syncthreads();
+        for (int k = t; k < ROOT_SLOTS; k += ROOT_TB) {
+            const int32_t rep = skey[k];
+            if (rep < 0) continue;
+            atomicMax(&c.rootedge[rep], smax[k]);
+            if (ssum[k]) atomicAdd(&c.csize[rep], ssum[k]);
+            if (smin[k] != NONE) atomicMin(&c.cmin[rep], smin[k]);
         }
-        if (act && !same) {
-            atomicMax(&c.rootedge[rep], (int32_t)r);
-            if (sz) atomicAdd(&c.csize[rep], sz);
-            if (mi != NONE) atomicMin(&c.cmin[rep], mi);
-        }
+        __syncthreads();
     }
 }
 
@@ -326,7 +355,7 @@ __global__ void fl_jump(int32_t *__restrict__ up, int64_t m, const int *__restri
             ch = 1;
         }
     }
-    if (__ballot(ch) && (threadIdx.x & 63) == 0) atomicOr(flag_next, 1);
+    flag_or(flag_next, ch);
 }
 
 struct NodeArr {
@@ -544,7 +573,7 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         HIP_CHECK(rocprim::exclusive_scan(tmp, tb, keep, pos, 0, (size_t)ne, rocprim::plus<int32_t>(), st));
         hipLaunchKernelGGL(fl_compact, dim3(grid_for(ne)), dim3(256), 0, st, va, vb, w, ne, keep, pos, m, ca, cb, cw,
                            m_dev);
-        hipLaunchKernelGGL(fl_order, dim3(grid_for(ne)), dim3(256), 0, st, cw, m_dev, flags);
+        hipLaunchKernelGGL(fl_order, dim3(grid_for(ne) / 4 + 1), dim3(1024), 0, st, cw, m_dev, flags);
     }
     HIP_CHECK(hipMemcpyAsync(pin, words, sizeof(int64_t) * 3, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
@@ -593,7 +622,7 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         const int gl = grid_for(nl);
         hipLaunchKernelGGL(dc_init, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
         hipLaunchKernelGGL(dc_unite, dim3(gl), dim3(256), 0, st, dc, b, nl, err);
-        hipLaunchKernelGGL(dc_root, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
+        hipLaunchKernelGGL(dc_root, dim3(gl), dim3(ROOT_TB), 0, st, dc, b, j, nl);
         hipLaunchKernelGGL(dc_link, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
     }
 
@@ -628,7 +657,8 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     auto jump_all = [&](int32_t *up) {  // roots of an upward forest, in place
         HIP_CHECK(hipMemsetAsync(jflags, 0, sizeof(int) * 64, st));
         for (int k = 0; k < rounds; k++)
-            hipLaunchKernelGGL(fl_jump, dim3(g), dim3(256), 0, st, up, m, k ? jflags + k - 1 : nullptr, jflags + k);
+            hipLaunchKernelGGL(fl_jump, dim3(g / 4 + 1), dim3(1024), 0, st, up, m, k ? jflags + k - 1 : nullptr,
+                               jflags + k);
     };
 
     hipLaunchKernelGGL(fl_tie_up, dim3(g), dim3(256), 0, st, dc.parent, ew, m, top, err);

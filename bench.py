@@ -2,15 +2,19 @@
 
     "Synthetic Gaussian blobs 1M x 3, exact HDBSCAN* (no sampling) on one MI355X, FP64"
 
-One step = the exact MR-HDBSCAN* leaf path over one 1M x 3 partition already resident in
-HBM: core distances (K1t: exact k-NN over minPts = 4 on the Morton/BVH index -- the lists
-are bit-identical to the all-pairs scan) -> mutual-reachability MST (K2b Boruvka; n-1 tree
-edges + n self edges as FirstStep emits them) -> the reducers' merge (stable descending
-sort, SortMST).  With N GPUs (torchrun, one process per GPU) every
-rank owns its own 1M-point partition (weak scaling, as MR-HDBSCAN* shards partitions) and the
-merge all-gathers every rank's edge list over RCCL before the sort.
+One step = the whole job for one 1M x 3 partition, end to end as SURVEY.md §8(d) defines it:
+parsed points in (pinned) host memory -> H2D -> core distances (K1t: exact k-NN over minPts =
+4 on the Morton/BVH index, bit-identical to the all-pairs scan) -> mutual-reachability MST (K2b
+Boruvka; n-1 tree edges + n self edges as FirstStep emits them) -> the reducers' merge (stable
+descending sort, SortMST) -> global HDBSCAN* hierarchy + flat labels (K6, minClSize 4) ->
+merged edge list and labels back in host memory.  With N GPUs (torchrun, one process per GPU)
+every rank owns its own 1M-point partition (weak scaling, as MR-HDBSCAN* shards partitions):
+each rank labels its partition, and the merge all-gathers every rank's edge list over RCCL
+before the sort (rank 0 copies the merged list out).
 
-Prints ONE JSON line (rank 0).  value = points/s over all ranks.
+Prints ONE JSON line (rank 0).  value = points/s over all ranks, end to end;
+device_resident_points_per_s = the same pipeline from HBM-resident points to HBM-resident
+merged edges (no transfers, no labels).
 """
 from __future__ import annotations
 
@@ -30,9 +34,13 @@ PKG = "232-hierarchical-density-based-clustering-using-mapreduce_amd"
 N_POINTS = 1_000_000
 D = 3
 MIN_PTS = 4
+MIN_CL_SIZE = 4
 CENTERS = 20
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector, FMA counted as 2 flops (spec)
 FP64_NOFMA_TOPS = 39.3   # non-FMA issue ceiling (256 CU x 2.4 GHz x 64 lanes)
+HBM_PEAK_GBS = 8000.0
+MALL_HIT_NS = 227.0      # MI355X_MICROARCH.md: global_load Infinity Cache hit latency (one lane, idle)
+WAVE_SLOTS = 256 * 4 * 4  # resident waves of the K2b scan: 256 CUs x 4 SIMDs x 4 waves (127 VGPRs)
 
 
 def make_blobs(n, d, centers, seed):
@@ -42,41 +50,68 @@ def make_blobs(n, d, centers, seed):
     return C[lab] + rng.normal(0, 1.0, size=(n, d))
 
 
-def cpu_baseline(X, budget_s=20.0):
-    """Oracle (line-faithful C restatement, -O2, 1 thread) on a bounded sample of the same
-    workload: k-NN core distances for R query rows against all n rows (n^2 work per
-    point, extrapolated linearly in rows) + reference Prim on an m-point prefix
-    (extrapolated by (n/m)^2).  points/s = n / (t_knn_full + t_prim_full)."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(X, budget_s=10.0):
+    """Oracle (line-faithful C restatement, -O2) on a bounded sample of the same workload:
+    k-NN core distances for R query rows against all n rows (n^2 work per point,
+    extrapolated linearly in rows) + reference Prim on an m-point prefix (extrapolated by
+    (n/m)^2); points/s = n / (t_knn_full + t_prim_full).  Timed twice: CPU-all (OpenMP over
+    query rows and over each Prim step's scan, OMP_NUM_THREADS threads -- Spark local[*]'s
+    stand-in) and one thread (what the reference runs at level 0).  The
+    labels step (O(n log n)) is left out of both: < 0.01 % of the O(n^2) work."""
     from oracle import oracle as O
     O.lib()
     n = X.shape[0]
-    rows = np.arange(0, n, max(1, n // 64))[:64]
-    t0 = time.perf_counter()
-    O.core_rows(X, rows, MIN_PTS, excl_self=True)
-    t_rows = time.perf_counter() - t0
-    # grow the row sample to ~half the budget
-    r2 = int(min(n, max(len(rows), len(rows) * (0.5 * budget_s) / max(t_rows, 1e-3))))
-    rows2 = np.linspace(0, n - 1, r2).astype(np.int64)
-    t0 = time.perf_counter()
-    O.core_rows(X, rows2, MIN_PTS, excl_self=True)
-    t_knn = (time.perf_counter() - t0) * (n / len(rows2))
-    m = 4000
-    Xm = X[:m]
-    core = O.core_distances(Xm, MIN_PTS, semantics=O.EXCL_SELF)
-    t0 = time.perf_counter()
-    O.prim_mst(Xm, core)
-    t_p = time.perf_counter() - t0
-    m2 = int(min(40000, m * max(1.0, (0.4 * budget_s / max(t_p, 1e-3)) ** 0.5)))
-    Xm = X[:m2]
-    core = O.core_rows(Xm, np.arange(m2), MIN_PTS, excl_self=True)
-    t0 = time.perf_counter()
-    O.prim_mst(Xm, core)
-    t_prim = (time.perf_counter() - t0) * (n / m2) ** 2
-    total = t_knn + t_prim
-    return {"value": n / total, "unit": "points/s", "cores": 1, "kind": "port",
-            "sample": f"oracle C -O2 1 thread: kNN of {len(rows2)} query rows vs all {n} rows "
-                      f"(x{n / len(rows2):.0f}) + reference Prim on a {m2}-point prefix "
-                      f"(x{(n / m2) ** 2:.0f}); extrapolated full step {total:.0f} s"}
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+
+    def sample(T, budget):
+        core_rows = (lambda Xs, r: O.core_rows(Xs, r, MIN_PTS)) if T == 1 else \
+            (lambda Xs, r: O.core_rows_par(Xs, r, MIN_PTS, T))
+        rows = np.arange(0, n, max(1, n // (64 * T)))[:64 * T]
+        t0 = time.perf_counter()
+        core_rows(X, rows)
+        t_rows = time.perf_counter() - t0
+        r2 = int(min(n, max(len(rows), len(rows) * (0.5 * budget) / max(t_rows, 1e-3))))
+        rows2 = np.linspace(0, n - 1, r2).astype(np.int64)
+        t0 = time.perf_counter()
+        core_rows(X, rows2)
+        t_knn = (time.perf_counter() - t0) * (n / len(rows2))
+        prim = (lambda Xs, c: O.prim_mst(Xs, c, self_edges=False)) if T == 1 else \
+            (lambda Xs, c: O.prim_mst_par(Xs, c, T))
+        m = 4000
+        core = O.core_rows(X[:m], np.arange(m), MIN_PTS)
+        t0 = time.perf_counter()
+        prim(X[:m], core)
+        t_p = time.perf_counter() - t0
+        m2 = int(min(60000, m * max(1.0, (0.4 * budget / max(t_p, 1e-3)) ** 0.5)))
+        Xm = X[:m2]
+        core = O.core_rows_par(Xm, np.arange(m2), MIN_PTS, threads)
+        t0 = time.perf_counter()
+        prim(Xm, core)
+        t_prim = (time.perf_counter() - t0) * (n / m2) ** 2
+        total = t_knn + t_prim
+        return total, len(rows2), m2
+
+    tot_all, r_all, m_all = sample(threads, budget_s)
+    tot_1, r_1, m_1 = sample(1, budget_s)
+    return {"value": n / tot_all, "unit": "points/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "sample": f"oracle C -O2, OpenMP {threads} threads: kNN of {r_all} query rows vs all {n} rows "
+                      f"(x{n / r_all:.0f}) + reference Prim (parallel scan per step) on a {m_all}-point prefix "
+                      f"(x{(n / m_all) ** 2:.0f}); extrapolated full step {tot_all:.0f} s",
+            "single_thread": {"value": n / tot_1, "cores": 1,
+                              "sample": f"kNN of {r_1} rows (x{n / r_1:.0f}) + Prim on a {m_1}-point prefix "
+                                        f"(x{(n / m_1) ** 2:.0f}); extrapolated full step {tot_1:.0f} s"}}
 
 
 def main():
@@ -86,8 +121,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=N_POINTS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--split", action="store_true",
-                    help="two calls (core distances, then Boruvka on a second index) instead of the fused leaf")
     args = ap.parse_args()
 
     import torch
@@ -100,117 +133,180 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     pkg = importlib.import_module(PKG)
-    from importlib import import_module
-    par = import_module(PKG + ".parallel")
+    par = importlib.import_module(PKG + ".parallel")
 
     n = args.n
     X_host = make_blobs(n, D, CENTERS, seed=1 + rank)
-    X = torch.from_numpy(X_host).cuda()
+    X_pin = torch.from_numpy(X_host).pin_memory()      # parsed points in host memory
+    X_dev = torch.empty(X_pin.shape, dtype=X_pin.dtype, device="cuda")
+    X_res = X_pin.cuda()                               # HBM-resident copy (device-only line)
+    ne_local = 2 * n - 1
+    ne_out = world * ne_local if rank == 0 else 0
+    va_h = torch.empty(ne_out, dtype=torch.int32).pin_memory()
+    vb_h = torch.empty(ne_out, dtype=torch.int32).pin_memory()
+    w_h = torch.empty(ne_out, dtype=torch.float64).pin_memory()
+    lab_h = torch.empty(n, dtype=torch.int32).pin_memory()
     ctx = pkg.Context.get(local)
     ctx.use_torch_stream()
     star = pkg.HDBSCANStar(ctx)
+    n_clusters = [0]
 
-    def leaf():
-        if args.split:
-            core = star.calculateCoreDistances(X, MIN_PTS, None, pkg.CORE_EXCL_SELF)
-            return core, star.constructMSTBoruvka(X, core, True)
-        return star.exactMST(X, MIN_PTS, None, pkg.CORE_EXCL_SELF, True)
+    def leaf(X):
+        _, mst = star.exactMST(X, MIN_PTS, None, pkg.CORE_EXCL_SELF, True)
+        return mst.getVerticeA(), mst.getVericeB(), mst.getEges()
 
-    def step():
-        _, mst = leaf()
-        va, vb, w = mst.getVerticeA(), mst.getVericeB(), mst.getEges()
+    def merge(va, vb, w):
         if world > 1:
             return par.merge_local_msts(va, vb, w)
         return pkg.sort_edges_desc(va, vb, w, ctx)
+
+    def step_e2e():
+        X_dev.copy_(X_pin, non_blocking=True)                    # H2D
+        va, vb, w = leaf(X_dev)
+        if world > 1:                                            # label this partition
+            la, lb, lw = pkg.sort_edges_desc(va.clone(), vb.clone(), w.clone(), ctx)
+            lab, n_clusters[0] = pkg.flat_labels(la, lb, lw, n, MIN_CL_SIZE, ctx=ctx)
+            ma, mb, mw = merge(va, vb, w)
+        else:
+            ma, mb, mw = merge(va, vb, w)
+            lab, n_clusters[0] = pkg.flat_labels(ma, mb, mw, n, MIN_CL_SIZE, ctx=ctx)
+        if rank == 0:                                            # D2H: merged list + labels
+            va_h.copy_(ma, non_blocking=True)
+            vb_h.copy_(mb, non_blocking=True)
+            w_h.copy_(mw, non_blocking=True)
+        lab_h.copy_(lab, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+
+    def step_dev():
+        return merge(*leaf(X_res))
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
+    def max_over_ranks(x):
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     for _ in range(args.warmup):
-        step()
+        step_e2e()
     barrier()
     # per-kernel device times: HIP events recorded on the launch stream inside the timed
     # region (measured cost of the records: ~1% of a step)
+    keys = ("knn_tree", "boruvka_total", "boruvka_scan", "merge_sort", "flat_labels")
     ctx.set_timing(True)
-    for k in ("knn_tree", "knn_sq", "boruvka_total", "boruvka_scan", "merge_sort", "exact_leaf_total"):
+    for k in keys:
         ctx.kernel_time(k)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = step()
+        step_e2e()
     barrier()
-    dt = time.perf_counter() - t0
+    dt = max_over_ranks(time.perf_counter() - t0)
     ctx.set_timing(False)
+    kt = {k: ctx.kernel_time(k) for k in keys}
+    # the same pipeline from HBM-resident points to HBM-resident merged edges
+    step_dev()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step_dev()
+    barrier()
+    dt_dev = max_over_ranks(time.perf_counter() - t0)
     tsteps = args.steps
-    knn_ms, knn_n = ctx.kernel_time("knn_tree")
-    bor_ms, bor_n = ctx.kernel_time("boruvka_total")
-    scan_ms, scan_n = ctx.kernel_time("boruvka_scan")
-    srt_ms, srt_n = ctx.kernel_time("merge_sort")
-    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    ms_step = dt * 1e3 / args.steps
-    # executed work (diagnostic pass outside the timed region): pairs each traversal evaluated
+
+    # checks on the last end-to-end step's host outputs
+    if rank == 0:
+        w_np = w_h.numpy()
+        assert w_np.shape[0] == world * ne_local and np.all(w_np[:-1] >= w_np[1:]), "merged list not descending"
+        if world == 1:
+            from scipy.sparse import coo_matrix
+            from scipy.sparse.csgraph import connected_components
+            a, b = va_h.numpy(), vb_h.numpy()
+            t = a != b
+            assert int(t.sum()) == n - 1, "not n-1 tree edges"
+            k, _ = connected_components(coo_matrix((np.ones(n - 1), (a[t], b[t])), shape=(n, n)), directed=False)
+            assert k == 1, "tree edges do not span the points"
+    lab_np = lab_h.numpy()
+    assert lab_np.min() >= 0 and lab_np.max() == n_clusters[0]
+
+    # executed work (diagnostic pass outside the timed region): per-round traversal stats
     ctx.set_option("count_evals", 1)
-    leaf()
+    leaf(X_res)
     knn_evals = ctx.get_stat("knn_tree_evals")
     bor_evals = ctx.get_stat("boruvka_evals")
+    rounds = []
+    for r in range(64):
+        try:
+            visits = ctx.get_stat(f"boruvka_r{r}_nodes") + ctx.get_stat(f"boruvka_r{r}_leaves")
+            waves = ctx.get_stat(f"boruvka_r{r}_active_waves")
+        except Exception:
+            break
+        rounds.append((visits, waves))
     ctx.set_option("count_evals", 0)
 
-    # sanity: the merged list is sorted descending and has N*(2n-1) edges
-    w_out = out[2]
-    assert w_out.shape[0] == world * (2 * n - 1)
     total_points = world * n
-    value = total_points * args.steps / dt
-    evals = world * (n * n + n * (n - 1) / 2)  # kNN n^2 + MST n(n-1)/2 (SURVEY §8(d))
-    # roofline of the dominant kernel (per launch, HIP events on the launch stream)
-    kern = {"knn_tree": (knn_ms, knn_n, knn_evals * tsteps), "boruvka_scan": (scan_ms, scan_n, bor_evals * tsteps)}
-    dom = max(kern, key=lambda k: kern[k][0])
-    k_ms, k_n, k_ev = kern[dom]
-    avg_s = k_ms / max(k_n, 1) / 1e3
-    flops_per_launch = 3 * D * (k_ev / max(k_n, 1))  # executed pair evals x 3d flops
-    achieved = flops_per_launch / avg_s / 1e12 if avg_s > 0 else 0.0
-    algo_flops = 3 * D * (n * n if dom == "knn_tree" else n * (n - 1) / 2) / max(k_n / tsteps, 1)
+    value = total_points * tsteps / dt
+    ms = {k: v[0] / tsteps for k, v in kt.items()}
+    scan_ms, scan_n = kt["boruvka_scan"]
+    avg_scan_s = scan_ms / max(scan_n, 1) / 1e3
+    # Latency roofline of the dominant kernel (the K2b scan): every node or leaf visit needs
+    # at least one dependent round trip to the index (L2/Infinity-Cache resident, MALL-hit
+    # latency), and a round can keep at most min(its waves, resident wave slots) of them in
+    # flight.  Lower bound per round = visits x latency / min(waves, slots); frac = the sum of
+    # those bounds / the measured scan time.
+    t_min = sum(v * MALL_HIT_NS * 1e-9 / max(1, min(w, WAVE_SLOTS)) for v, w in rounds if v)
+    visits = sum(v for v, _ in rounds)
+    scan_s_step = scan_ms / tsteps / 1e3
+    achieved = visits / scan_s_step if scan_s_step > 0 else 0.0
+    peak = visits / t_min if t_min > 0 else 0.0
     traffic = None
-    # HBM bytes per launch from the committed rocprofv3 PMC passes (tools/profile_bench.sh,
-    # FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), keyed by kernel symbol
     pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    sym = {"knn_tree": "knn_tree_kernel", "boruvka_scan": "boruvka_bvh_kernel"}[dom]
-    if os.path.exists(pmc):
+    if os.path.exists(pmc):  # HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, tools/profile_bench.sh)
         with open(pmc) as fh:
-            traffic = json.load(fh).get(sym, {}).get("hbm_bytes_per_launch")
+            traffic = json.load(fh).get("boruvka_bvh_kernel", {}).get("hbm_bytes_per_launch")
+    fp64_tflops = 3 * D * (bor_evals / max(scan_n / tsteps, 1)) / avg_scan_s / 1e12 if avg_scan_s > 0 else 0.0
+    evals = world * (n * n + n * (n - 1) / 2)  # kNN n^2 + MST n(n-1)/2 (SURVEY §8(d))
     line = {
         "metric": "points/sec end-to-end + mutual-reach distance evals/sec at 1/2/4/8 GPUs",
         "value": value,
         "unit": "points/s",
         "n_gpus": world,
-        "steps": args.steps,
+        "steps": tsteps,
         "warmup": args.warmup,
-        "ms_per_step": ms_step,
+        "ms_per_step": dt * 1e3 / tsteps,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded Gaussian blobs, 20 centers ~U[-100,100]^3, sigma 1, seed 1+rank)",
-        "config": {"workload": "config 2: blobs 1M x 3 exact HDBSCAN* (no sampling), minPts 4",
-                   "points_per_gpu": n, "d": D, "min_pts": MIN_PTS, "core": "EXCL_SELF",
-                   "mst": "boruvka (exact; Prim-identical sorted weights)"
-                   + (" on a second index" if args.split else ", kNN-seeded round 0 on the K1t index"), "merge": "stable desc sort",
+        "config": {"workload": "config 2: blobs 1M x 3 exact HDBSCAN* (no sampling), minPts 4, minClSize 4",
+                   "points_per_gpu": n, "d": D, "min_pts": MIN_PTS, "min_cl_size": MIN_CL_SIZE,
+                   "core": "EXCL_SELF", "timed": "pinned host X -> H2D -> K1t cores -> K2b MST + self edges "
+                   "-> merge sort -> K6 flat labels -> D2H of the merged list and labels",
                    "parallelism": f"partition-sharded x{world}"},
-        "mrd_evals_per_s": evals * args.steps / dt,
-        "kernels_ms_per_step": {"knn_tree": knn_ms / tsteps, "boruvka_total": bor_ms / tsteps,
-                                "boruvka_scan": scan_ms / tsteps, "merge_sort": srt_ms / tsteps},
+        "n_clusters": n_clusters[0],
+        "device_resident_points_per_s": total_points * tsteps / dt_dev,
+        "device_resident_ms_per_step": dt_dev * 1e3 / tsteps,
+        "mrd_evals_per_s": evals * tsteps / dt,
+        "kernels_ms_per_step": ms,
         "executed_pair_evals_per_step": {"knn_tree": knn_evals, "boruvka_scan": bor_evals,
                                          "algorithmic": n * n + n * (n - 1) // 2},
-        "roofline": {"bound": "fp64-valu", "kernel": dom, "achieved": achieved,
-                     "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
-                     "traffic": traffic, "work": "executed pair evals x 3d flops (pruned traversal)",
-                     "flops_per_launch": flops_per_launch, "avg_launch_ms": avg_s * 1e3,
-                     "launches_per_step": k_n / tsteps,
-                     "algorithmic_equiv_tflops": algo_flops / avg_s / 1e12},
+        "roofline": {"bound": "latency", "kernel": "boruvka_scan (boruvka_bvh_kernel)",
+                     "unit": "node visits/s", "achieved": achieved, "peak": peak,
+                     "frac": achieved / peak if peak else 0.0, "traffic": traffic,
+                     "model": f"per round: visits x {MALL_HIT_NS:.0f} ns (one dependent Infinity-Cache "
+                              f"round trip per visit) / min(waves, {WAVE_SLOTS} resident wave slots)",
+                     "visits_per_step": visits, "rounds": [[v, w] for v, w in rounds],
+                     "avg_launch_ms": avg_scan_s * 1e3, "launches_per_step": scan_n / tsteps,
+                     "fp64": {"achieved_tflops": fp64_tflops, "peak": FP64_PEAK_TFLOPS,
+                              "frac": fp64_tflops / FP64_PEAK_TFLOPS,
+                              "work": "executed pair evals x 3d flops"},
+                     "hbm": {"achieved_gbs": (traffic or 0) / avg_scan_s / 1e9 if avg_scan_s > 0 else 0.0,
+                             "peak": HBM_PEAK_GBS}},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(X_host)

@@ -977,3 +977,115 @@ int orc_core_rows(const double *X, int64_t n, int d, const int64_t *rows, int64_
     free(buf);
     return ORC_OK;
 }
+
+/* ------------------------------------------------ CPU-all baseline (bench.py only)
+ * the line-faithful loops above, with OpenMP over independent units standing
+ * in for Spark local[*].  Results are identical to the serial functions: each query row is
+ * independent (orc_core_rows), and the Prim step's parallel scan combines per-thread
+ * candidates with the reference select rule (smaller value; equal values -> larger index,
+ * HDBSCANStar.java:177-180 '<='), the update rule (:170-173) being per-vertex. */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+int orc_core_rows_par(const double *X, int64_t n, int d, const int64_t *rows, int64_t nr, int min_pts, int metric,
+                      int excl_self, int nthreads, double *core) {
+    if (min_pts < 2 || nthreads < 1) return ORC_EINVAL;
+    int K = min_pts - 1;
+    int rc = ORC_OK;
+#pragma omp parallel num_threads(nthreads)
+    {
+        double *buf = (double *)malloc(sizeof(double) * K);
+        if (!buf) {
+#pragma omp atomic write
+            rc = ORC_ENOMEM;
+        }
+#pragma omp for schedule(dynamic, 4)
+        for (int64_t r = 0; r < nr; r++) {
+            if (!buf) continue;
+            int64_t p = rows[r];
+            for (int i = 0; i < K; i++) buf[i] = JMAX;
+            for (int64_t q = 0; q < n; q++) {
+                if (excl_self && p == q) continue;
+                knn_insert(buf, K, orc_distance(X + p * d, X + q * d, d, metric));
+            }
+            core[r] = buf[K - 1];
+        }
+        free(buf);
+    }
+    return rc;
+}
+
+int orc_prim_mst_par(const double *X, int64_t n, int d, const double *core, int metric, int nthreads, int32_t *va,
+                     int32_t *vb, double *w) {
+    if (n < 1 || d <= 0 || nthreads < 1) return ORC_EINVAL;
+    unsigned char *attached = (unsigned char *)calloc((size_t)n, 1);
+    int32_t *parent = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+    double *best = (double *)malloc(sizeof(double) * (size_t)n);
+    double *cand_d = (double *)malloc(sizeof(double) * (size_t)nthreads);
+    int64_t *cand_i = (int64_t *)malloc(sizeof(int64_t) * (size_t)nthreads);
+    if (!attached || !parent || !best || !cand_d || !cand_i) {
+        free(attached); free(parent); free(best); free(cand_d); free(cand_i);
+        return ORC_ENOMEM;
+    }
+    for (int64_t i = 0; i < n; i++) best[i] = JMAX;
+    best[n - 1] = 0;
+    int64_t cur = n - 1;
+    attached[n - 1] = 1;
+    int rc = ORC_OK;
+#pragma omp parallel num_threads(nthreads)
+    {
+        int t = 0, T = 1;
+#ifdef _OPENMP
+        t = omp_get_thread_num();
+        T = omp_get_num_threads();
+#endif
+        const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+        for (int64_t step = 1; step < n; step++) {
+            const int64_t c = cur;  /* read after the previous step's barrier */
+            double nd = JMAX;
+            int64_t np = -1;
+            for (int64_t nb = lo; nb < hi; nb++) {
+                if (c == nb || attached[nb]) continue;
+                double mrd = orc_distance(X + c * d, X + nb * d, d, metric);
+                if (core[c] > mrd) mrd = core[c];
+                if (core[nb] > mrd) mrd = core[nb];
+                if (mrd < best[nb]) {
+                    best[nb] = mrd;
+                    parent[nb] = (int32_t)c;
+                }
+                if (best[nb] <= nd) {
+                    nd = best[nb];
+                    np = nb;
+                }
+            }
+            cand_d[t] = nd;
+            cand_i[t] = np;
+#pragma omp barrier
+#pragma omp single
+            {
+                double bd = JMAX;
+                int64_t bi = -1;
+                for (int k = 0; k < T; k++)  /* ascending ranges: '<=' keeps the last minimum */
+                    if (cand_i[k] >= 0 && cand_d[k] <= bd) {
+                        bd = cand_d[k];
+                        bi = cand_i[k];
+                    }
+                if (bi < 0) rc = ORC_EREF_OOB;
+                else {
+                    attached[bi] = 1;
+                    cur = bi;
+                }
+            } /* implicit barrier */
+            if (rc != ORC_OK) break;
+        }
+    }
+    if (rc == ORC_OK)
+        for (int64_t i = 0; i < n - 1; i++) {
+            va[i] = parent[i];
+            vb[i] = (int32_t)i;
+            w[i] = best[i];
+        }
+    free(attached); free(parent); free(best); free(cand_d); free(cand_i);
+    return rc;
+}

@@ -64,6 +64,8 @@ def lib():
         L.orc_quicksort_edges.argtypes = [ip, ip, dp, i64]
         L.orc_merge_edges.argtypes = [ip, ip, dp, i64]
         L.orc_core_rows.argtypes = [dp, i64, i32, lp, i64, i32, i32, i32, dp]
+        L.orc_core_rows_par.argtypes = [dp, i64, i32, lp, i64, i32, i32, i32, i32, dp]
+        L.orc_prim_mst_par.argtypes = [dp, i64, i32, dp, i32, i32, ip, ip, dp]
         L.orc_local_model.argtypes = [dp, dp, i64, i32, i32, i32, i32, ip, ip, ip, dp, ip, ip, dp, lp]
         _lib = L
     return _lib
@@ -113,6 +115,31 @@ def core_rows(X, rows, min_pts, metric="euclidean", excl_self=True):
     _chk(lib().orc_core_rows(px, n, d, rows.ctypes.data_as(C.POINTER(C.c_int64)), rows.shape[0], min_pts,
                              _metric(metric), int(excl_self), _d(out)[1]), "core_rows")
     return out
+
+
+def core_rows_par(X, rows, min_pts, nthreads, metric="euclidean", excl_self=True):
+    """core_rows with OpenMP over the query rows (bench.py CPU-all baseline); same values."""
+    X, px = _d(X)
+    n, d = X.shape
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    out = np.empty(rows.shape[0], np.float64)
+    _chk(lib().orc_core_rows_par(px, n, d, rows.ctypes.data_as(C.POINTER(C.c_int64)), rows.shape[0], min_pts,
+                                 _metric(metric), int(excl_self), int(nthreads), _d(out)[1]), "core_rows_par")
+    return out
+
+
+def prim_mst_par(X, core, nthreads, metric="euclidean"):
+    """orc_prim_mst (identity ids, no self edges) with an OpenMP-parallel scan per Prim step
+    (bench.py CPU-all baseline); the same edges as prim_mst."""
+    X, px = _d(X)
+    n, d = X.shape
+    core, pc = _d(core)
+    va = np.zeros(n - 1, np.int32)
+    vb = np.zeros(n - 1, np.int32)
+    w = np.zeros(n - 1, np.float64)
+    _chk(lib().orc_prim_mst_par(px, n, d, pc, _metric(metric), int(nthreads), _i(va)[1], _i(vb)[1], _d(w)[1]),
+         "prim_mst_par")
+    return va, vb, w
 
 
 def knn_lists(X, min_pts, metric="euclidean", excl_self=False):

@@ -243,3 +243,19 @@ def test_oracle_bubble_slice_against_golden(oracle):
 def test_skin_parse_d1():
     X = load_skin(5)
     assert X.shape == (5, 3) and X[0].tolist() == [74.0, 85.0, 123.0]
+
+
+def test_cpu_all_variants_equal_serial(oracle):
+    """bench.py's CPU-all baseline (OpenMP over rows / over each Prim step's scan) computes
+    exactly what the serial oracle does, ties included (Skin duplicates)."""
+    from conftest import load_skin
+    for X in (blobs(3000, 3, 6, 2), load_skin(2500)):
+        n = X.shape[0]
+        rows = np.arange(0, n, 7)
+        ref = oracle.core_rows(X, rows, 4)
+        core = oracle.core_distances(X, 4, semantics=oracle.EXCL_SELF)
+        va, vb, w = oracle.prim_mst(X, core, self_edges=False)
+        for t in (1, 3, 8):
+            assert np.array_equal(oracle.core_rows_par(X, rows, 4, t), ref)
+            pa, pb, pw = oracle.prim_mst_par(X, core, t)
+            assert np.array_equal(pa, va) and np.array_equal(pb, vb) and np.array_equal(pw, w)
