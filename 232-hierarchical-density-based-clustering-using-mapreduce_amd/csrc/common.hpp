@@ -56,6 +56,8 @@ struct hdb_ctx {
     std::map<std::string, std::pair<double, int64_t>> acc;
     hdb::Arena arenas[12];
     int64_t *pinned = nullptr;  // pinned_words(): async device -> host counters
+    void *host_stage = nullptr;  // host_arena(): grow-only pinned staging
+    size_t host_stage_bytes = 0;
     int num_cus = 256;
     bool force_fp64 = false;  // disable the FP32 screen in K1 (A/B and tests)
     bool knn_tree = true;     // K1t (box-pruned) for euclidean lists when the shape allows
@@ -85,6 +87,8 @@ enum {
 void *arena(hdb_ctx *ctx, int slot, size_t bytes);
 constexpr int PINNED_WORDS = 512;
 int64_t *pinned_words(hdb_ctx *ctx);
+// grow-only pinned host buffer (synchronises the stream before it grows)
+void *host_arena(hdb_ctx *ctx, size_t bytes);
 // order `to` after all work queued so far on `from` (event record + stream wait)
 void stream_fence(hdb_ctx *ctx, hipStream_t from, hipStream_t to);
 

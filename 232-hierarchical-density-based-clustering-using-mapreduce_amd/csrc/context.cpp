@@ -13,6 +13,20 @@ int64_t *pinned_words(hdb_ctx *ctx) {
     return ctx->pinned;
 }
 
+void *host_arena(hdb_ctx *ctx, size_t bytes) {
+    if (ctx->host_stage_bytes < bytes) {
+        if (ctx->host_stage) {
+            HIP_CHECK(hipStreamSynchronize(ctx->stream));
+            HIP_CHECK(hipHostFree(ctx->host_stage));
+            ctx->host_stage = nullptr;
+        }
+        size_t nb = bytes + bytes / 4 + 4096;
+        HIP_CHECK(hipHostMalloc(&ctx->host_stage, nb));
+        ctx->host_stage_bytes = nb;
+    }
+    return ctx->host_stage;
+}
+
 void *arena(hdb_ctx *ctx, int slot, size_t bytes) {
     Arena &a = ctx->arenas[slot];
     if (bytes == 0) bytes = 16;
@@ -165,6 +179,7 @@ void hdb_ctx_destroy(hdb_ctx *ctx) {
     for (auto &a : ctx->arenas)
         if (a.ptr) (void)hipFree(a.ptr);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->host_stage) (void)hipHostFree(ctx->host_stage);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->side) {
         (void)hipStreamSynchronize(ctx->side);

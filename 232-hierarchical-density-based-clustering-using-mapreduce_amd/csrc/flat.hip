@@ -29,6 +29,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <numeric>
 
 #include "common.hpp"
@@ -56,30 +57,37 @@ __device__ __forceinline__ uint32_t uf_prio(int32_t x, int64_t n) {
     return (x >= n ? 0x80000000u : 0u) | (h >> 1);
 }
 
-__device__ __forceinline__ int32_t uf_find(int32_t *uf, int32_t x) {
-    volatile int32_t *u = uf;
+// label records: {uf parent, root edge, size, min id} in 16 bytes (one transaction per label)
+struct __align__(16) LRec {
+    int32_t uf, rootedge, csize, cmin;
+};
+
+__device__ __forceinline__ int32_t uf_find(LRec *lr, int32_t x) {
+    volatile int32_t *u = &lr->uf;  // stride 4 ints
     while (true) {
-        int32_t p = u[x];
+        int32_t p = u[4 * (int64_t)x];
         if (p == x) return x;
-        int32_t g = u[p];
+        int32_t g = u[4 * (int64_t)p];
         if (g == p) return p;
-        u[x] = g;  // path halving: g is an ancestor of x
+        u[4 * (int64_t)x] = g;  // path halving: g is an ancestor of x
         x = g;
     }
 }
 
-__device__ __forceinline__ bool uf_unite(int32_t *uf, int32_t a, int32_t b, int64_t n) {
+// returns the root this union hooked (every label but its component's final root is hooked
+// exactly once), or -1 when a and b were already connected
+__device__ __forceinline__ int32_t uf_unite(LRec *uf, int32_t a, int32_t b, int64_t n) {
     while (true) {
         a = uf_find(uf, a);
         b = uf_find(uf, b);
-        if (a == b) return false;
+        if (a == b) return -1;
         const uint32_t pa = uf_prio(a, n), pb = uf_prio(b, n);
         if (pa < pb || (pa == pb && a < b)) {
             int32_t t = a;
             a = b;
             b = t;
         }
-        if (atomicCAS(&uf[b], b, a) == b) return true;  // b hooks under the higher-priority a
+        if (atomicCAS(&uf[b].uf, b, a) == b) return b;  // b hooks under the higher-priority a
     }
 }
 
@@ -200,11 +208,9 @@ __device__ __forceinline__ int64_t l_rank(int64_t i, int b) {
 
 struct DC {
     int32_t *lab;       // 2m endpoint labels (vertex id < n, or n + root edge rank)
-    int32_t *uf;        // n + m
-    int32_t *stamp;     // n + m: 2j = initialised at depth j, 2j+1 = size counted
-    int32_t *rootedge;  // n + m: largest L edge of the component (at its representative)
-    int32_t *csize;     // n + m
-    int32_t *cmin;      // n + m
+    LRec *lr;           // n + m label records
+    int32_t *stamp;     // n + m: 2j = a label of an L edge at depth j
+    int32_t *hooked;    // m: the label an L edge's union hooked (-1: none)
     int32_t *parent;    // m: parent edge rank (NONE: root)
     int32_t *esize;     // m: |C(e)|
     int32_t *eminid;    // m: smallest point id in C(e)
@@ -218,11 +224,8 @@ __global__ void dc_init(DC c, int b, int j, int64_t nl) {
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             int32_t x = c.lab[2 * r + s];
-            c.uf[x] = x;
+            c.lr[x] = LRec{x, -1, 0, NONE};  // rootedge: largest L edge of the component
             c.stamp[x] = 2 * j;
-            c.rootedge[x] = -1;
-            c.csize[x] = 0;
-            c.cmin[x] = NONE;
         }
     }
 }
@@ -231,7 +234,9 @@ __global__ void dc_unite(DC c, int b, int64_t nl, int *__restrict__ err) {
     HDB_GRID_STRIDE(i, nl) {
         int64_t r = l_rank(i, b);
         if (r >= c.m) continue;
-        if (!uf_unite(c.uf, c.lab[2 * r], c.lab[2 * r + 1], c.n)) atomicOr(err, FE_CYCLE);  // rare: bad input
+        const int32_t h = uf_unite(c.lr, c.lab[2 * r], c.lab[2 * r + 1], c.n);
+        c.hooked[r] = h;
+        if (h < 0) atomicOr(err, FE_CYCLE);  // rare: bad input
     }
 }
 
@@ -268,18 +273,12 @@ __global__ __launch_bounds__(ROOT_TB) void dc_root(DC c, int b, int j, int64_t n
         const int64_t i = base + t;
         const int64_t r = i < nl ? l_rank(i, b) : c.m;
         if (r < c.m) {
-            const int32_t rep = uf_find(c.uf, c.lab[2 * r]);
-            int32_t sz = 0, mi = NONE;
-#pragma unroll
-            for (int s = 0; s < 2; s++) {
-                int32_t x = c.lab[2 * r + s];
-                // first to count label x (plain read first: a shared label is claimed once)
-                if (((volatile int32_t *)c.stamp)[x] == 2 * j &&
-                    atomicCAS(&c.stamp[x], 2 * j, 2 * j + 1) == 2 * j) {
-                    sz += x < c.n ? 1 : c.esize[x - c.n];
-                    mi = min(mi, x < c.n ? x : c.eminid[x - c.n]);
-                }
-            }
+            const int32_t rep = uf_find(c.lr, c.lab[2 * r]);
+            // the label this edge hooked is counted once, here; the final root label is
+            // added by its root edge in dc_link
+            const int32_t x = c.hooked[r];
+            const int32_t sz = x < 0 ? 0 : (x < c.n ? 1 : c.esize[x - c.n]);
+            const int32_t mi = x < 0 ? NONE : (x < c.n ? x : c.eminid[x - c.n]);
             uint32_t h = uf_prio(rep, 0) & (ROOT_SLOTS - 1);
             while (true) {  // <= ROOT_TB distinct keys in 2x slots: always finds one
                 int32_t k = atomicCAS(&skey[h], -1, rep);
@@ -294,9 +293,9 @@ __global__ __launch_bounds__(ROOT_TB) void dc_root(DC c, int b, int j, int64_t n
         for (int k = t; k < ROOT_SLOTS; k += ROOT_TB) {
             const int32_t rep = skey[k];
             if (rep < 0) continue;
-            atomicMax(&c.rootedge[rep], smax[k]);
-            if (ssum[k]) atomicAdd(&c.csize[rep], ssum[k]);
-            if (smin[k] != NONE) atomicMin(&c.cmin[rep], smin[k]);
+            atomicMax(&c.lr[rep].rootedge, smax[k]);
+            if (ssum[k]) atomicAdd(&c.lr[rep].csize, ssum[k]);
+            if (smin[k] != NONE) atomicMin(&c.lr[rep].cmin, smin[k]);
         }
         __syncthreads();
     }
@@ -307,10 +306,11 @@ __global__ void dc_link(DC c, int b, int j, int64_t nl) {
         int64_t r = l_rank(i, b);
         if (r >= c.m) continue;
         {  // L edge: a component root records |C(e)| and its smallest id
-            const int32_t rep = uf_find(c.uf, c.lab[2 * r]);
-            if (c.rootedge[rep] == (int32_t)r) {
-                c.esize[r] = c.csize[rep];
-                c.eminid[r] = c.cmin[rep];
+            const int32_t rep = uf_find(c.lr, c.lab[2 * r]);
+            const LRec q = c.lr[rep];
+            if (q.rootedge == (int32_t)r) {
+                c.esize[r] = q.csize + (rep < c.n ? 1 : c.esize[rep - c.n]);
+                c.eminid[r] = min(q.cmin, rep < c.n ? rep : c.eminid[rep - c.n]);
             }
         }
         const int64_t u = r | (int64_t(1) << b);  // the U edge paired with this thread
@@ -318,12 +318,80 @@ __global__ void dc_link(DC c, int b, int j, int64_t nl) {
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             int32_t x = c.lab[2 * u + s];
-            if (c.stamp[x] == 2 * j + 1) {  // x lies in an L component of this block
-                const int32_t R = c.rootedge[uf_find(c.uf, x)];
-                atomicMin(&c.parent[R], (int32_t)u);
+            if (c.stamp[x] == 2 * j) {  // x lies in an L component of this block
+                const int32_t R = c.lr[uf_find(c.lr, x)].rootedge;
+                // lighter U edges run in earlier lanes: most see their bound already beaten
+                if (((volatile int32_t *)c.parent)[R] > (int32_t)u) atomicMin(&c.parent[R], (int32_t)u);
                 c.lab[2 * u + s] = (int32_t)(c.n + R);
             }
         }
+    }
+}
+
+// Deep depths in one launch: a block of LOC_EDGES consecutive ranks whose labels name the
+// components of F_{<lo} runs the sequential Kruskal process itself (one wave per block, the
+// block's labels hashed to LDS slots, union by size, one lane walking the ranks in order):
+// parents inside the block, |C(e)| and min id of C(e) for every edge.  Parents that leave the
+// block were assigned by the shallower depths.
+constexpr int LOC_LOG = 8, LOC_EDGES = 1 << LOC_LOG, LOC_SLOTS = 4 * LOC_EDGES;
+__global__ __launch_bounds__(64) void dc_local(DC c, int *__restrict__ err) {
+    __shared__ int32_t key[LOC_SLOTS], lsz[LOC_SLOTS], lmn[LOC_SLOTS];
+    __shared__ int16_t luf[LOC_SLOTS], lre[LOC_SLOTS];
+    __shared__ int16_t le[2 * LOC_EDGES];
+    const int lane = threadIdx.x;
+    for (int64_t lo = (int64_t)blockIdx.x * LOC_EDGES; lo < c.m; lo += (int64_t)gridDim.x * LOC_EDGES) {
+        const int cnt = (int)(c.m - lo < LOC_EDGES ? c.m - lo : LOC_EDGES);
+        for (int k = lane; k < LOC_SLOTS; k += 64) key[k] = -1;
+        __syncthreads();
+        for (int k = lane; k < 2 * cnt; k += 64) {
+            const int32_t x = c.lab[2 * lo + k];
+            uint32_t h = uf_prio(x, 0) & (LOC_SLOTS - 1);
+            while (true) {  // <= 2 LOC_EDGES keys in 4x slots
+                const int32_t old = atomicCAS(&key[h], -1, x);
+                if (old == -1) {  // inserted: initialise the slot
+                    luf[h] = (int16_t)h;
+                    lre[h] = -1;
+                    lsz[h] = x < c.n ? 1 : c.esize[x - c.n];
+                    lmn[h] = x < c.n ? x : c.eminid[x - c.n];
+                    break;
+                }
+                if (old == x) break;
+                h = (h + 1) & (LOC_SLOTS - 1);
+            }
+            le[k] = (int16_t)h;
+        }
+        __syncthreads();
+        if (lane == 0) {
+            auto find = [&](int x) {
+                while (luf[x] != x) {
+                    const int g = luf[luf[x]];
+                    luf[x] = (int16_t)g;
+                    x = g;
+                }
+                return x;
+            };
+            for (int k = 0; k < cnt; k++) {
+                int a = find(le[2 * k]), b = find(le[2 * k + 1]);
+                if (a == b) {
+                    atomicOr(err, FE_CYCLE);
+                    break;
+                }
+                if (lre[a] >= 0) c.parent[lo + lre[a]] = (int32_t)(lo + k);
+                if (lre[b] >= 0) c.parent[lo + lre[b]] = (int32_t)(lo + k);
+                if (lsz[a] < lsz[b]) {
+                    const int t = a;
+                    a = b;
+                    b = t;
+                }
+                luf[b] = (int16_t)a;
+                lsz[a] += lsz[b];
+                lmn[a] = min(lmn[a], lmn[b]);
+                lre[a] = (int16_t)k;
+                c.esize[lo + k] = lsz[a];
+                c.eminid[lo + k] = lmn[a];
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -533,7 +601,9 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         cv.take<int32_t>(mm);            // eb
         cv.take<double>(mm);             // ew
         cv.take<int32_t>(2 * mm);        // lab
-        for (int k = 0; k < 5; k++) cv.take<int32_t>(n + mm);  // uf stamp rootedge csize cmin
+        cv.take<LRec>(n + mm);           // label records
+        cv.take<int32_t>(n + mm);        // stamp
+        cv.take<int32_t>(mm);            // hooked
         for (int k = 0; k < 3; k++) cv.take<int32_t>(mm);      // parent esize eminid
         cv.take<int32_t>(n);             // pparent
     };
@@ -550,11 +620,9 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     double *ew = cv.take<double>(mm);
     DC dc;
     dc.lab = cv.take<int32_t>(2 * mm);
-    dc.uf = cv.take<int32_t>(n + mm);
+    dc.lr = cv.take<LRec>(n + mm);
     dc.stamp = cv.take<int32_t>(n + mm);
-    dc.rootedge = cv.take<int32_t>(n + mm);
-    dc.csize = cv.take<int32_t>(n + mm);
-    dc.cmin = cv.take<int32_t>(n + mm);
+    dc.hooked = cv.take<int32_t>(mm);
     dc.parent = cv.take<int32_t>(mm);
     dc.esize = cv.take<int32_t>(mm);
     dc.eminid = cv.take<int32_t>(mm);
@@ -614,7 +682,8 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     // ---- 2. Kruskal tree by rank divide and conquer
     int J = 0;
     while ((int64_t(1) << J) <= m) J++;  // 2^J > m: every rank < m has a clear bit below J
-    for (int j = 0; j < J; j++) {
+    // global depths split blocks down to LOC_EDGES ranks; dc_local finishes each such block
+    for (int j = 0; j < J - LOC_LOG; j++) {
         const int b = J - 1 - j;
         // L ranks (bit b clear) below m; every U rank is an L rank + 2^b
         const int64_t blk = int64_t(1) << (b + 1), half = int64_t(1) << b;
@@ -625,10 +694,12 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         hipLaunchKernelGGL(dc_root, dim3(gl), dim3(ROOT_TB), 0, st, dc, b, j, nl);
         hipLaunchKernelGGL(dc_link, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
     }
+    hipLaunchKernelGGL(dc_local, dim3((int)std::min<int64_t>(ceil_div(m, LOC_EDGES), 65536)), dim3(64), 0, st, dc, err);
 
     // ---- 3. multi-way nodes, condensation
     // reuse the union-find scratch (n + m ints each) for the node arrays
-    int32_t *top = dc.uf, *pnode = dc.stamp, *nvalid = dc.rootedge, *vsum = dc.csize, *is_start = dc.cmin;
+    int32_t *top = (int32_t *)dc.lr, *pnode = top + (n + m), *nvalid = pnode + (n + m), *vsum = nvalid + (n + m),
+            *is_start = dc.stamp;
     Carver nc2{nullptr, 0};
     nc2.take<int32_t>(m);  // cup / cs
     nc2.take<int32_t>(m);  // cid
@@ -701,56 +772,70 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     hipLaunchKernelGGL(fl_seg, dim3(g), dim3(256), 0, st, key2, m, seg, seg_hi);
     hipLaunchKernelGGL(fl_stab, dim3((int)std::min<int64_t>(K, 65536)), dim3(64), 0, st, val2, seg, seg_hi, K, stab);
     hipLaunchKernelGGL(fl_cluster_meta, dim3(g), dim3(256), 0, st, is_start, cid, cs, pnode, dc.eminid, m, cpar, cminid);
-    std::vector<int32_t> hpar(K), hmin(K), hlab(K, 0);
-    std::vector<double> hstab(K);
-    HIP_CHECK(hipMemcpyAsync(hpar.data(), cpar, sizeof(int32_t) * K, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(hmin.data(), cminid, sizeof(int32_t) * K, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(hstab.data(), stab, sizeof(double) * K, hipMemcpyDeviceToHost, st));
+    // pinned staging: [stab K doubles][par K][min K][lab K]
+    char *hs = (char *)host_arena(ctx, (size_t)K * 20);
+    double *hstab = (double *)hs;
+    int32_t *hpar = (int32_t *)(hs + (size_t)K * 8), *hmin = hpar + K, *hlab = hmin + K;
+    HIP_CHECK(hipMemcpyAsync(hpar, cpar, sizeof(int32_t) * K, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(hmin, cminid, sizeof(int32_t) * K, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(hstab, stab, sizeof(double) * K, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
+    const auto t_host0 = std::chrono::steady_clock::now();
+    std::fill(hlab, hlab + K, 0);
 
     // FOSC (flat.cpp step 3) over the K clusters: ids ascend with the start node's rank, so a
-    // child cluster always precedes its parent; the root is K-1
-    std::vector<int32_t> koff(K + 1, 0), kids(K);
+    // child cluster always precedes its parent; the root is K-1.  Scratch is per thread and
+    // reused (fresh pages cost more than the O(K) work).
+    static thread_local std::vector<int32_t> koff, kids, fillp, sel;
+    static thread_local std::vector<double> contrib;
+    static thread_local std::vector<char> flg;  // bit 0: self-selected, 1: chosen, 2: blocked
+    koff.assign((size_t)K + 1, 0);
+    kids.resize((size_t)K);
     for (int32_t c = 0; c < K - 1; c++) koff[hpar[c] + 1]++;
     for (int32_t c = 0; c < K; c++) koff[c + 1] += koff[c];
-    {
-        std::vector<int32_t> fill(koff.begin(), koff.end() - 1);
-        for (int32_t c = 0; c < K - 1; c++) kids[fill[hpar[c]]++] = c;
-    }
-    for (int32_t c = 0; c < K; c++)
-        std::sort(kids.begin() + koff[c], kids.begin() + koff[c + 1],
-                  [&](int32_t a, int32_t b) { return hmin[a] < hmin[b]; });
-    std::vector<double> contrib(K, 0.0);
-    std::vector<char> self_sel(K, 0);
+    fillp.assign(koff.begin(), koff.end() - 1);
+    for (int32_t c = 0; c < K - 1; c++) kids[fillp[hpar[c]]++] = c;
+    contrib.resize((size_t)K);
+    flg.assign((size_t)K, 0);
     for (int32_t c = 0; c < K - 1; c++) {
+        const int32_t k0 = koff[c], k1 = koff[c + 1];
+        if (k1 - k0 > 1)
+            std::sort(kids.begin() + k0, kids.begin() + k1, [&](int32_t a, int32_t b) { return hmin[a] < hmin[b]; });
         double prop = 0.0;
-        for (int32_t k = koff[c]; k < koff[c + 1]; k++) prop = prop + contrib[kids[k]];
-        if (koff[c + 1] == koff[c] || hstab[c] >= prop) {  // Cluster.propagate: ties keep the parent
+        for (int32_t k = k0; k < k1; k++) prop = prop + contrib[kids[k]];
+        if (k1 == k0 || hstab[c] >= prop) {  // Cluster.propagate: ties keep the parent
             contrib[c] = hstab[c];
-            self_sel[c] = 1;
+            flg[c] = 1;
         } else {
             contrib[c] = prop;
         }
     }
-    std::vector<int32_t> sel, todo(kids.begin() + koff[K - 1], kids.begin() + koff[K]);
-    while (!todo.empty()) {
-        int32_t c = todo.back();
-        todo.pop_back();
-        if (self_sel[c]) sel.push_back(c);
-        else todo.insert(todo.end(), kids.begin() + koff[c], kids.begin() + koff[c + 1]);
+    // selected = self-selected with no selected ancestor below the root (top-down = descending id)
+    sel.clear();
+    for (int32_t c = K - 2; c >= 0; c--) {
+        const int32_t p = hpar[c];
+        const bool blocked = p != K - 1 && (flg[p] & 6);
+        if (blocked) flg[c] |= 4;
+        else if (flg[c] & 1) {
+            flg[c] |= 2;
+            sel.push_back(c);
+        }
     }
     std::sort(sel.begin(), sel.end(), [&](int32_t a, int32_t b) { return hmin[a] < hmin[b]; });
     for (size_t i = 0; i < sel.size(); i++) hlab[sel[i]] = (int32_t)(i + 1);
-    // every cluster takes the label of its nearest selected ancestor-or-self (parents have
-    // larger ids: top-down is descending id); the root keeps 0
+    // every cluster takes the label of its nearest selected ancestor-or-self; the root keeps 0
     for (int32_t c = K - 2; c >= 0; c--)
-        if (hlab[c] == 0) hlab[c] = hlab[hpar[c]];    HIP_CHECK(hipMemcpyAsync(clab, hlab.data(), sizeof(int32_t) * K, hipMemcpyHostToDevice, st));
+        if (hlab[c] == 0) hlab[c] = hlab[hpar[c]];
+    ctx->stats["flat_host_us"] =
+        std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t_host0).count();
+    HIP_CHECK(hipMemcpyAsync(clab, hlab, sizeof(int32_t) * K, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(fl_point_labels, dim3(grid_for(n)), dim3(256), 0, st, pparent, top, cs, cid, clab, n,
                        labels);
     HIP_CHECK(hipGetLastError());
-    // hlab is read by the queued copy: wait before it goes out of scope
+    // the pinned staging is rewritten by the next call: wait for the queued copy
     HIP_CHECK(hipStreamSynchronize(st));
     if (n_clusters) *n_clusters = (int64_t)sel.size();
+    ctx->stats["flat_clusters_total"] = K;  // condensed-tree clusters incl. the root
 }
 
 }  // namespace hdb
