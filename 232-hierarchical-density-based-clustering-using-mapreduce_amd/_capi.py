@@ -104,6 +104,12 @@ def lib():
             "hdb_quicksort_edges": [ip, ip, dp, i64],
             "hdb_sort_edges_desc": [vp, ip, ip, dp, i64],
             "hdb_flat_labels": [vp, ip, ip, dp, i64, i64, i32, ip, lp],
+            "hdb_comm_unique_id": [vp, i32],
+            "hdb_comm_init": [vp, i32, i32, vp, C.POINTER(vp)],
+            "hdb_free": [vp],
+            "hdb_copy": [vp, vp, vp, i64],
+            "hdb_merge_edges": [vp, ip, ip, dp, lp, i64, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp),
+                                C.POINTER(C.c_int64)],
             "hdb_format_double": [C.c_double, C.c_char_p, i32],
             "hdb_parse_points": [C.c_char_p, i64, i32, i32, dp, i64, lp, ip],
             "hdb_format_mst_records": [ip, ip, dp, ip, ip, ip, i64, vp, i64, lp],
@@ -115,6 +121,8 @@ def lib():
             f.restype = C.c_int
         L.hdb_ctx_destroy.argtypes = [vp]
         L.hdb_ctx_destroy.restype = None
+        L.hdb_comm_destroy.argtypes = [vp]
+        L.hdb_comm_destroy.restype = None
         L.hdb_last_error.restype = C.c_char_p
         L.hdb_version.restype = C.c_int
         _lib = L
@@ -127,7 +135,8 @@ EXPORTED = ["hdb_ctx_create", "hdb_ctx_destroy", "hdb_ctx_set_stream", "hdb_ctx_
             "hdb_leaf_msts", "hdb_mst_boruvka", "hdb_exact_mst", "hdb_nearest_sample", "hdb_bubble_stats",
             "hdb_bubble_core_distances", "hdb_bubble_prim_mst", "hdb_local_model", "hdb_quicksort_edges",
             "hdb_sort_edges_desc", "hdb_flat_labels", "hdb_format_double", "hdb_parse_points",
-            "hdb_format_mst_records", "hdb_parse_mst_records"]
+            "hdb_format_mst_records", "hdb_parse_mst_records", "hdb_comm_unique_id", "hdb_comm_init",
+            "hdb_comm_destroy", "hdb_free", "hdb_copy", "hdb_merge_edges"]
 
 
 def check(rc: int, what: str):

@@ -20,6 +20,16 @@ oracle for the parity tests):
           CombineStep (D5 fold order) -> per subset LocalModelReduceByKey (D4) -> partition
           induction (Main.java:272-289, including the in-place relabel) -> LabelClassification
   merge   UnionFindReducer + SortMST: stable descending sort of the iteration-major edge list
+
+Multi-GPU (one process per GPU, torch.distributed initialised, X given to
+every rank): the plan is computed identically on every rank -- leaves go to ranks by LPT on
+n_i^2, the big subsets' points are split in contiguous chunks for the nearest-sample scan (the
+assignments are all-gathered), bubble statistics are recomputed on every rank (the D5 fold
+order keeps them bit-exact), local models go to ranks by LPT on b_i^2 (results all-gathered
+and applied in subset order), and the merge places every local edge at its position in the
+single-device concatenation (hdb_merge_edges over the library's RCCL communicator under
+nccl, torch.distributed under gloo) before the stable sort.  Every rank returns the same
+result as one device does.
 """
 from __future__ import annotations
 
@@ -28,6 +38,7 @@ import math
 import numpy as np
 
 from . import _capi as A
+from . import parallel as P
 from .hdbscanstar import metric_of
 
 LEAF_PRIM_MAX = 65536  # leaves up to this size run the exact reference Prim (batched; one
@@ -54,7 +65,7 @@ class MRHDBSCANStar:
 
     def __init__(self, minPts=4, minClSize=4, processing_units=50, k=0.2, samples_per_subset=None,
                  seed=20210101, distanceFunction=None, all_inter_edges=True, max_levels=64, ctx=None,
-                 device=0, flat_labels=True, profile=False, exact_prim_leaves=False):
+                 device=0, flat_labels=True, profile=False, exact_prim_leaves=False, group=None):
         self.minPts = minPts
         self.minClSize = minClSize
         self.processing_units = processing_units
@@ -73,6 +84,8 @@ class MRHDBSCANStar:
         # forced leaves above LEAF_PRIM_MAX use Boruvka where it applies (same weights,
         # topology may differ among equal-weight edges)
         self.exact_prim_leaves = exact_prim_leaves
+        self.group = group      # torch.distributed group (None: the default group, if any)
+        self._comm = None       # HdbComm for the merge under nccl
         self.timings = {}
         self._t0 = None
 
@@ -156,11 +169,12 @@ class MRHDBSCANStar:
         self.timings = {}
         self._t0 = None
         self._mark(None)
+        world, rank = P.world_rank(self.group)
         key_of = torch.zeros(n, dtype=torch.int64, device=dev)
         alive = torch.arange(n, dtype=torch.int64, device=dev)  # ids in the current _unprocessed_ file
         forced = set()
         leaf_of = torch.full((n,), -1, dtype=torch.int64, device=dev)
-        edge_lists, levels = [], []
+        blocks, block_size, levels = [], {}, []  # blocks: (canonical id, edges) computed here
         iteration, processed, next_id = 0, 0, 2  # Main.java:103-105
         while processed < n:
             # group the alive records by (key, global id) -- D5
@@ -183,7 +197,13 @@ class MRHDBSCANStar:
                          big={k: cnt for k, _, cnt in big}, labels={}, new_keys={})
             if leaf_k:
                 self._mark("bookkeeping")
-                edge_lists.extend(self._leaves(X, leaf_rows, leaf_k))
+                owner = P.lpt([int(r.shape[0]) ** 2 for r in leaf_rows], world)
+                mine = [i for i in range(len(leaf_k)) if owner[i] == rank]
+                if mine:
+                    got = self._leaves(X, [leaf_rows[i] for i in mine], [leaf_k[i] for i in mine])
+                    blocks.extend(((iteration, 0, i), e) for i, e in zip(mine, got))
+                for i, r in enumerate(leaf_rows):
+                    block_size[(iteration, 0, i)] = 2 * int(r.shape[0]) - 1
                 self._mark("leaves")
                 for kk, r in zip(leaf_k, leaf_rows):
                     leaf_of[r] = kk
@@ -205,10 +225,14 @@ class MRHDBSCANStar:
             s_key = torch.cat(s_key)
             Xb = X.index_select(0, brows).contiguous()
             S = X.index_select(0, s_gid).contiguous()
-            nearest = torch.empty(brows.shape[0], dtype=torch.int32, device=dev)
-            A.check(A.lib().hdb_nearest_sample(c.h, Xb.data_ptr(), Xb.shape[0], S.data_ptr(), S.shape[0], d,
-                                               self.metric, bkey_local.data_ptr(), s_key.data_ptr(),
-                                               nearest.data_ptr(), None), "FirstStep.nearest")
+            lo, hi = P.chunk(brows.shape[0], world, rank)  # this rank's points (all of them at N = 1)
+            nearest = torch.empty(hi - lo, dtype=torch.int32, device=dev)
+            if hi > lo:
+                A.check(A.lib().hdb_nearest_sample(c.h, Xb[lo:hi].data_ptr(), hi - lo, S.data_ptr(), S.shape[0], d,
+                                                   self.metric, bkey_local[lo:hi].data_ptr(), s_key.data_ptr(),
+                                                   nearest.data_ptr(), None), "FirstStep.nearest")
+            if world > 1:
+                nearest = P.allgather_var(nearest, self.group)
             self._mark("nearest_sample")
             # nearest is the list position in S (keyed: within the point's own subset)
             nb = S.shape[0]
@@ -222,27 +246,48 @@ class MRHDBSCANStar:
             self._mark("bubbles")
             s_gid_h = s_gid.cpu().numpy()
             new_key_of_bubble = np.full(nb, -2, np.int64)
-            inter = []
+            # local models: LPT over the ranks on b^2, results gathered, applied in subset order
+            nonempty_of = [np.nonzero(info_h[s_off[i]:s_off[i + 1], 2] > 0)[0] for i in range(len(big))]  # D4
+            owner = P.lpt([int(ne.shape[0]) ** 2 for ne in nonempty_of], world)
+            results = {}
             for i, (kk, s0, cnt) in enumerate(big):
+                if owner[i] != rank:
+                    continue
                 a, b = s_off[i], s_off[i + 1]
-                nonempty = np.nonzero(info_h[a:b, 2] > 0)[0]  # D4
-                labels = None
+                nonempty = nonempty_of[i]
+                res = (None, None, None)
                 if nonempty.shape[0] >= 2:
                     try:
-                        labels, iedges = self._local_model(rep_h[a:b][nonempty], info_h[a:b][nonempty])
+                        labels, (iva, ivb, iw) = self._local_model(rep_h[a:b][nonempty], info_h[a:b][nonempty])
                     except A.HdbError as e:  # D10
-                        level.setdefault("model_errors", {})[kk] = e.code
-                        labels = None
+                        res = (None, e.code, None)
                     else:
-                        iva, ivb, iw = iedges
+                        inter = None
                         if iw.shape[0]:
                             gid = s_gid_h[a:b][nonempty].astype(np.int32)
-                            if self.all_inter_edges:  # D7
-                                inter.append((gid[iva], gid[ivb], iw))
-                            else:
-                                inter.append((iva[:1], ivb[:1], iw[:1]))
+                            inter = (gid[iva], gid[ivb], iw) if self.all_inter_edges else (iva[:1], ivb[:1], iw[:1])
+                        res = (labels, None, inter)
+                results[i] = res
+            if world > 1:
+                for part in P.allgather_object(results, self.group):
+                    results.update(part)
+            inter_i = 0
+            for i, (kk, s0, cnt) in enumerate(big):
+                a = s_off[i]
+                nonempty = nonempty_of[i]
+                labels, code, inter = results[i]
+                if code is not None:
+                    level.setdefault("model_errors", {})[kk] = code
+                if inter is not None:  # D7 block: kept by the rank that computed the model
+                    bid = (iteration - 1, 1, inter_i)
+                    block_size[bid] = int(inter[2].shape[0])
+                    if owner[i] == rank:
+                        blocks.append((bid, tuple(torch.from_numpy(np.ascontiguousarray(x, dt)).to(dev) for x, dt in
+                                                  zip(inter, (np.int32, np.int32, np.float64)))))
+                    inter_i += 1
                 if labels is None:
                     labels = np.full(nonempty.shape[0], 2, np.int32)
+                labels = np.array(labels, np.int32)
                 level["labels"][kk] = labels.copy()
                 for cl in sorted(set(labels.tolist())):  # Main.java:272-289 (in-place relabel)
                     labels[labels == cl] = next_id
@@ -256,18 +301,29 @@ class MRHDBSCANStar:
             self._mark("local_models")
             tbl = torch.from_numpy(new_key_of_bubble).to(dev)
             key_of[brows] = tbl[nearest.long()]
-            for va, vb, w in inter:
-                edge_lists.append((torch.from_numpy(np.ascontiguousarray(va, np.int32)).to(dev),
-                                   torch.from_numpy(np.ascontiguousarray(vb, np.int32)).to(dev),
-                                   torch.from_numpy(np.ascontiguousarray(w, np.float64)).to(dev)))
             alive = brows
             levels.append(level)
         self._mark("bookkeeping")
-        # UnionFindReducer + SortMST: stable descending sort of the concatenation
-        va = torch.cat([e[0] for e in edge_lists]) if edge_lists else torch.zeros(0, dtype=torch.int32, device=dev)
-        vb = torch.cat([e[1] for e in edge_lists]) if edge_lists else torch.zeros(0, dtype=torch.int32, device=dev)
-        w = torch.cat([e[2] for e in edge_lists]) if edge_lists else torch.zeros(0, dtype=torch.float64, device=dev)
-        if w.shape[0]:
+        # UnionFindReducer + SortMST: stable descending sort of the iteration-major
+        # concatenation (leaf blocks in key order, then the level's inter-cluster blocks)
+        order = sorted(block_size)
+        off, pos = {}, 0
+        for bid in order:
+            off[bid] = pos
+            pos += block_size[bid]
+        blocks.sort(key=lambda t: t[0])
+        cat = lambda i, dt: (torch.cat([e[i] for _, e in blocks]) if blocks
+                             else torch.zeros(0, dtype=dt, device=dev))
+        va, vb, w = cat(0, torch.int32), cat(1, torch.int32), cat(2, torch.float64)
+        if world > 1:
+            seq = torch.cat([torch.arange(off[bid], off[bid] + block_size[bid], dtype=torch.int64, device=dev)
+                             for bid, _ in blocks]) if blocks else torch.zeros(0, dtype=torch.int64, device=dev)
+            import torch.distributed as dist
+            if self._comm is None and dist.get_backend(self.group) == "nccl":
+                self._comm = P.HdbComm(c, self.group)
+            va, vb, w = P.merge_local_msts(va.contiguous(), vb.contiguous(), w.contiguous(), self.group, seq=seq,
+                                           comm=self._comm)
+        elif w.shape[0]:
             A.check(A.lib().hdb_sort_edges_desc(c.h, va.data_ptr(), vb.data_ptr(), w.data_ptr(), w.shape[0]),
                     "SortMST")
         out = dict(edges=(va, vb, w), levels=levels, leaf_of=leaf_of, iterations=iteration)

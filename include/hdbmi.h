@@ -186,6 +186,29 @@ int hdb_quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne);
  * sort).  The cross-GPU all-gather feeding it runs over RCCL in the host layer. */
 int hdb_sort_edges_desc(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne);
 
+/* ---------------------------------------------- cross-GPU merge over RCCL (§8(b), §8(e))
+ * One communicator per rank (one process per GPU).  The caller moves the unique id from the
+ * rank that made it to the others (Spark broadcast, torch.distributed, MPI ...). */
+typedef struct hdb_comm hdb_comm;
+/* Writes an RCCL unique id (128 bytes) into id_out; returns its size or an error. */
+int hdb_comm_unique_id(void *id_out, int32_t cap);
+/* Collective over the nranks ranks; the context fixes the device and stream. */
+int hdb_comm_init(hdb_ctx *ctx, int32_t nranks, int32_t rank, const void *id, hdb_comm **out);
+void hdb_comm_destroy(hdb_comm *comm);
+/* Frees a buffer the library allocated (hdb_merge_edges outputs). */
+int hdb_free(void *p);
+/* Copies bytes between any two host/device buffers on the context stream; synchronises. */
+int hdb_copy(hdb_ctx *ctx, void *dst, const void *src, int64_t bytes);
+/* Main.java:302-347 + UnionFindReducer.call + SortMST (UnionFindReducer.java:19-69,
+ * SortMST.java:9-17): every rank passes its local edge list; all ranks receive the merged
+ * list of all E edges (device memory allocated by the library, freed with hdb_free), stably
+ * sorted by DESCENDING weight.  seq (nullable; on every rank or on none): the canonical
+ * position of each local edge in the global concatenation (a permutation of [0, E) over all
+ * ranks) -- the sort then sees that concatenation, independent of which rank computed which
+ * partition; NULL = rank-major concatenation.  Collective; synchronises. */
+int hdb_merge_edges(hdb_comm *comm, const int32_t *va, const int32_t *vb, const double *w, const int64_t *seq,
+                    int64_t e_local, int32_t **va_all, int32_t **vb_all, double **w_all, int64_t *e_all);
+
 /* ------------------------------------------------ global flat labels (§8(f) #1)
  * The step the reference never completes (Main.java:351-408): HDBSCAN* hierarchy over the
  * merged MST and its flat FOSC / excess-of-mass partition -- HDBSCANStar.java:208-625

@@ -1,0 +1,128 @@
+"""Multi-GPU driver on the GPU box: 2 ranks (gloo process group, both on the
+box's one MI355X -- RCCL refuses two ranks on one device) run the sharded MR-HDBSCAN* loop
+(leaves by LPT, point-chunked nearest sample, local models by LPT, seq-ordered merge) and must
+return exactly what one device returns: the same levels, bubble labels, merged edge list
+(order included) and flat labels, on a C1-prefix (Skin, zero-weight ties) and a C3-shaped
+(d = 16, recursive sampling with an explicit per-subset sample count) input.
+
+The library's own RCCL communicator (hdb_comm_* / hdb_merge_edges, the C-ABI a Java driver
+binds) is exercised at world size 1 under an nccl process group: seq-ordered placement +
+stable descending sort must equal the reference merge of the canonical concatenation."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import blobs, load_skin
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    "skin_prefix": dict(data=lambda: load_skin(12000), processing_units=1500, k=0.05),
+    "c3_shaped": dict(data=lambda: blobs(24000, 16, 12, 3, spread=50.0), processing_units=3000,
+                      samples_per_subset=256),
+}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(pkg, X, case):
+    kw = {k: v for k, v in case.items() if k != "data"}
+    r = pkg.MRHDBSCANStar(minPts=4, minClSize=4, **kw).run(X)
+    lev = [(L["iteration"], sorted(L["leaves"].items()), sorted(L["big"].items()),
+            {k: np.asarray(v).tolist() for k, v in L["labels"].items()}, L["new_keys"], L.get("model_errors"))
+           for L in r["levels"]]
+    return dict(edges=[x.cpu().numpy() for x in r["edges"]], labels=r["labels"].cpu().numpy(),
+                n_clusters=r["n_clusters"], leaf_of=r["leaf_of"].cpu().numpy(), levels=lev, iterations=r["iterations"])
+
+
+def _worker(rank, world, port, name, out_dir):
+    import importlib
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pkg = importlib.import_module("232-hierarchical-density-based-clustering-using-mapreduce_amd")
+    res = _run(pkg, CASES[name]["data"](), CASES[name])
+    np.save(os.path.join(out_dir, f"r{rank}.npy"), np.array([res], dtype=object), allow_pickle=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_sharded_driver_equals_single_device(pkg, name, tmp_path):
+    ref = _run(pkg, CASES[name]["data"](), CASES[name])
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), name, str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        got = np.load(os.path.join(tmp_path, f"r{r}.npy"), allow_pickle=True)[0]  # written by this test
+        assert got["iterations"] == ref["iterations"] and got["levels"] == ref["levels"], r
+        assert np.array_equal(got["leaf_of"], ref["leaf_of"])
+        for a, b in zip(got["edges"], ref["edges"]):
+            assert np.array_equal(a, b), r
+        assert got["n_clusters"] == ref["n_clusters"] and np.array_equal(got["labels"], ref["labels"])
+
+
+def _comm_worker(rank, world, port, out_dir):
+    import importlib
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    pkg = importlib.import_module("232-hierarchical-density-based-clustering-using-mapreduce_amd")
+    P = importlib.import_module("232-hierarchical-density-based-clustering-using-mapreduce_amd.parallel")
+    ctx = pkg.Context.get(0)
+    ctx.use_torch_stream()
+    comm = P.HdbComm(ctx)
+    rng = np.random.default_rng(5)
+    E = 5000
+    va = rng.integers(0, 10**6, E).astype(np.int32)
+    vb = rng.integers(0, 10**6, E).astype(np.int32)
+    w = np.round(rng.uniform(0, 4, E), 1)  # heavy ties: order matters
+    seq = rng.permutation(E).astype(np.int64)
+    t = lambda x: torch.from_numpy(x).cuda()
+    a, b, ww = P.merge_local_msts(t(va), t(vb), t(w), seq=t(seq), comm=comm)
+    a2, b2, w2 = P.merge_local_msts(t(va), t(vb), t(w), comm=comm)
+    np.savez(os.path.join(out_dir, "comm.npz"), va=va, vb=vb, w=w, seq=seq, a=a.cpu().numpy(), b=b.cpu().numpy(),
+             ww=ww.cpu().numpy(), a2=a2.cpu().numpy(), b2=b2.cpu().numpy(), w2=w2.cpu().numpy())
+    bad = False
+    try:
+        P.merge_local_msts(t(va), t(vb), t(w), seq=t(np.zeros(E, np.int64)), comm=comm)
+    except pkg.HdbError:
+        bad = True
+    assert bad, "a non-permutation seq must be rejected"
+    comm.close()
+    dist.destroy_process_group()
+
+
+def test_hdb_merge_edges_rccl_world1(oracle, tmp_path):
+    mp.spawn(_comm_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
+    z = np.load(os.path.join(tmp_path, "comm.npz"))
+    inv = np.empty_like(z["seq"])
+    inv[z["seq"]] = np.arange(z["seq"].shape[0])
+    canon = [(z["va"][inv], z["vb"][inv], z["w"][inv])]
+    ref = oracle.merge_edges(canon)
+    assert np.array_equal(z["a"], ref[0]) and np.array_equal(z["b"], ref[1]) and np.array_equal(z["ww"], ref[2])
+    ref2 = oracle.merge_edges([(z["va"], z["vb"], z["w"])])
+    assert np.array_equal(z["a2"], ref2[0]) and np.array_equal(z["b2"], ref2[1]) and np.array_equal(z["w2"], ref2[2])
