@@ -65,7 +65,8 @@ class MRHDBSCANStar:
 
     def __init__(self, minPts=4, minClSize=4, processing_units=50, k=0.2, samples_per_subset=None,
                  seed=20210101, distanceFunction=None, all_inter_edges=True, max_levels=64, ctx=None,
-                 device=0, flat_labels=True, profile=False, exact_prim_leaves=False, group=None):
+                 device=0, flat_labels=True, profile=False, exact_prim_leaves=False, group=None,
+                 prim_leaf_max=LEAF_PRIM_MAX):
         self.minPts = minPts
         self.minClSize = minClSize
         self.processing_units = processing_units
@@ -84,6 +85,9 @@ class MRHDBSCANStar:
         # forced leaves above LEAF_PRIM_MAX use Boruvka where it applies (same weights,
         # topology may differ among equal-weight edges)
         self.exact_prim_leaves = exact_prim_leaves
+        # leaves up to this size run the reference Prim (exact topology, latency-bound: one
+        # step per point); larger ones K2b where it applies (exact weights, ties may differ)
+        self.prim_leaf_max = prim_leaf_max
         self.group = group      # torch.distributed group (None: the default group, if any)
         self._comm = None       # HdbComm for the merge under nccl
         self.timings = {}
@@ -114,7 +118,7 @@ class MRHDBSCANStar:
         out = []
         c = self._c()
         d = X.shape[1]
-        prim = lambda n: (n <= LEAF_PRIM_MAX or self.exact_prim_leaves
+        prim = lambda n: (n <= self.prim_leaf_max or self.exact_prim_leaves
                           or not boruvka_ok(self.metric, d, self.minPts))
         small = [(k, r) for k, r in zip(keys, rows_list) if prim(r.shape[0])]
         if small:

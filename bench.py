@@ -114,6 +114,88 @@ def cpu_baseline(X, budget_s=10.0):
                                         f"(x{(n / m_1) ** 2:.0f}); extrapolated full step {tot_1:.0f} s"}}
 
 
+PARTITIONED = {  # SURVEY.md §8(d) C3 / C5 (recursive sampling, data bubbles), strong scaling
+    "c3": dict(n=4_000_000, d=16, centers=50, spread=50.0, seed=3, samples_per_subset=4096, processing_units=65536,
+               desc="config 3: blobs 4M x 16, recursive sampling (4,096 samples/subset, pu 65,536)"),
+    "c5": dict(n=16_000_000, d=8, centers=100, spread=100.0, seed=5, samples_per_subset=16384,
+               processing_units=65536,
+               desc="config 5: blobs 16M x 8, data bubbles (16,384 samples/subset, pu 65,536), RCCL merge"),
+}
+
+
+def run_partitioned(args, workload):
+    """C3 / C5: the whole MR-HDBSCAN* job (every level, the merge, the flat labels) on N GPUs
+    with the sharded driver; every rank holds the parsed points (pinned host memory), the
+    timed region covers H2D, the job and the D2H of the merged list and labels.  Strong
+    scaling: the same job at every N; value = points / job time."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    pkg = importlib.import_module(PKG)
+    cfg = PARTITIONED[workload]
+    n = args.n if args.n != N_POINTS else cfg["n"]
+    rng = np.random.default_rng(cfg["seed"])
+    C = rng.uniform(-cfg["spread"], cfg["spread"], size=(cfg["centers"], cfg["d"]))
+    X_pin = torch.from_numpy(C[rng.integers(0, cfg["centers"], size=n)] +
+                             rng.normal(0, 1.0, size=(n, cfg["d"]))).pin_memory()
+    drv = pkg.MRHDBSCANStar(minPts=MIN_PTS, minClSize=MIN_CL_SIZE, processing_units=cfg["processing_units"],
+                            samples_per_subset=cfg["samples_per_subset"], prim_leaf_max=4096, profile=args.phases)
+    out = {}
+
+    def job():
+        Xd = X_pin.to("cuda", non_blocking=True)
+        r = drv.run(Xd)
+        if rank == 0:
+            out["edges"] = [x.to("cpu") for x in r["edges"]]
+            out["labels"] = r["labels"].to("cpu")
+        out["r"] = r
+        torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        job()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        job()
+    barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    r = out["r"]
+    if rank == 0:
+        w = out["edges"][2].numpy()
+        assert w.shape[0] == 2 * n - 1 and np.all(w[:-1] >= w[1:])
+        lv = r["levels"]
+        line = {"metric": "points/sec end-to-end + mutual-reach distance evals/sec at 1/2/4/8 GPUs",
+                "value": n * args.steps / dt, "unit": "points/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True,
+                "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+                "data": f"synthetic (seeded Gaussian blobs, seed {cfg['seed']})",
+                "config": {"workload": cfg["desc"], "points": n, "d": cfg["d"], "min_pts": MIN_PTS,
+                           "min_cl_size": MIN_CL_SIZE, "prim_leaf_max": 4096,
+                           "parallelism": f"sharded driver x{world} (leaves/local models by LPT, "
+                                          f"point-chunked nearest sample, RCCL merge)"},
+                "iterations": r["iterations"], "n_clusters": r["n_clusters"],
+                "levels": len(lv), "leaves": int(sum(len(L["leaves"]) for L in lv)),
+                "model_errors": int(sum(len(L.get("model_errors", {})) for L in lv)),
+                "phases_s": {k: round(v, 4) for k, v in drv.timings.items()} if args.phases else None,
+                "roofline": None}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -121,7 +203,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=N_POINTS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["c2", "c3", "c5"], default="c2",
+                    help="c2 (default): the per-GPU C2 pipeline (weak scaling); c3/c5: the whole "
+                         "partitioned job over the sharded driver (strong scaling)")
+    ap.add_argument("--phases", action="store_true", help="c3/c5: per-phase times (synchronising)")
     args = ap.parse_args()
+    if args.workload != "c2":
+        return run_partitioned(args, args.workload)
 
     import torch
     import torch.distributed as dist
