@@ -104,6 +104,7 @@ def lib():
             "hdb_quicksort_edges": [ip, ip, dp, i64],
             "hdb_sort_edges_desc": [vp, ip, ip, dp, i64],
             "hdb_flat_labels": [vp, ip, ip, dp, i64, i64, i32, ip, lp],
+            "hdb_local_mst_ids": [vp, ip, i64, ip, ip, i64, i32, ip, ip, ip],
             "hdb_comm_unique_id": [vp, i32],
             "hdb_comm_init": [vp, i32, i32, vp, C.POINTER(vp)],
             "hdb_free": [vp],
@@ -136,7 +137,7 @@ EXPORTED = ["hdb_ctx_create", "hdb_ctx_destroy", "hdb_ctx_set_stream", "hdb_ctx_
             "hdb_bubble_core_distances", "hdb_bubble_prim_mst", "hdb_local_model", "hdb_quicksort_edges",
             "hdb_sort_edges_desc", "hdb_flat_labels", "hdb_format_double", "hdb_parse_points",
             "hdb_format_mst_records", "hdb_parse_mst_records", "hdb_comm_unique_id", "hdb_comm_init",
-            "hdb_comm_destroy", "hdb_free", "hdb_copy", "hdb_merge_edges"]
+            "hdb_comm_destroy", "hdb_free", "hdb_copy", "hdb_merge_edges", "hdb_local_mst_ids"]
 
 
 def check(rc: int, what: str):

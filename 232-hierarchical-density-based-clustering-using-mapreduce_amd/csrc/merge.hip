@@ -20,6 +20,10 @@ __global__ void edge_keys_kernel(const double *__restrict__ w, int64_t ne, doubl
     }
 }
 
+__global__ void pos_fill_kernel(int32_t *__restrict__ p, int64_t n) {
+    HDB_GRID_STRIDE(i, n) p[i] = (int32_t)i;
+}
+
 __global__ void edge_gather_kernel(const int32_t *__restrict__ perm, int64_t ne, const int32_t *__restrict__ a_in,
                                    const int32_t *__restrict__ b_in, const double *__restrict__ w_in,
                                    int32_t *__restrict__ a_out, int32_t *__restrict__ b_out,
@@ -62,6 +66,88 @@ void sort_edges_desc_device(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, i
     HIP_CHECK(hipMemcpyAsync(vb, tb_, sizeof(int32_t) * ne, hipMemcpyDeviceToDevice, ctx->stream));
     HIP_CHECK(hipMemcpyAsync(w, tw, sizeof(double) * ne, hipMemcpyDeviceToDevice, ctx->stream));
     HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------ CreateLocalMST record fields
+// fake1 / fake2 of CreateLocalMST's records (CreateLocalMST.java:242,266,276-285) are the
+// partition-local indices of an edge's two vertices: the position of the global id in the
+// partition's `indices` array.  ids sorted once (radix), one binary search per endpoint.
+__global__ void local_ids_dup_kernel(const int32_t *__restrict__ keys, int64_t n, int *__restrict__ err) {
+    HDB_GRID_STRIDE(i, n - 1) {
+        if (keys[i] == keys[i + 1]) atomicOr(err, 1);
+    }
+}
+
+__device__ __forceinline__ int32_t local_of(const int32_t *keys, const int32_t *pos, int64_t n, int32_t id, int *err) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (keys[mid] < id) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo >= n || keys[lo] != id) {
+        atomicOr(err, 2);
+        return -1;
+    }
+    return pos[lo];
+}
+
+__global__ void local_ids_kernel(const int32_t *__restrict__ keys, const int32_t *__restrict__ pos, int64_t n,
+                                 const int32_t *__restrict__ va, const int32_t *__restrict__ vb, int64_t ne,
+                                 int32_t node, int32_t *__restrict__ f1, int32_t *__restrict__ f2,
+                                 int32_t *__restrict__ nd, int *__restrict__ err) {
+    HDB_GRID_STRIDE(e, ne) {
+        if (keys) {
+            f1[e] = local_of(keys, pos, n, va[e], err);
+            f2[e] = local_of(keys, pos, n, vb[e], err);
+        } else {
+            f1[e] = va[e];
+            f2[e] = vb[e];
+        }
+        if (nd) nd[e] = node;
+    }
+}
+
+void local_mst_ids_device(hdb_ctx *ctx, const int32_t *ids, int64_t n, const int32_t *va, const int32_t *vb, int64_t ne,
+                          int32_t node, int32_t *fake1, int32_t *fake2, int32_t *node_out) {
+    if (ne <= 0) return;
+    hipStream_t st = ctx->stream;
+    const int g = (int)std::min<int64_t>(ceil_div(ne, 256), 8192);
+    int32_t *keys = nullptr, *pos = nullptr;
+    int *err = nullptr;
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+        size_t o = off;
+        off += (bytes + 255) & ~size_t(255);
+        return o;
+    };
+    const size_t o_e = carve(sizeof(int) * 4), o_k = carve(sizeof(int32_t) * std::max<int64_t>(n, 1)),
+                 o_k2 = carve(sizeof(int32_t) * std::max<int64_t>(n, 1)), o_p = carve(sizeof(int32_t) * std::max<int64_t>(n, 1)),
+                 o_p2 = carve(sizeof(int32_t) * std::max<int64_t>(n, 1));
+    char *base = (char *)arena(ctx, A_WORK3, off);
+    err = (int *)(base + o_e);
+    HIP_CHECK(hipMemsetAsync(err, 0, sizeof(int) * 4, st));
+    if (ids) {
+        if (n > INT32_MAX) HDB_THROW(HDB_EINVAL, "too many vertices");
+        int32_t *k1 = (int32_t *)(base + o_k), *p1 = (int32_t *)(base + o_p);
+        keys = (int32_t *)(base + o_k2);
+        pos = (int32_t *)(base + o_p2);
+        HIP_CHECK(hipMemcpyAsync(k1, ids, sizeof(int32_t) * n, hipMemcpyDefault, st));
+        hipLaunchKernelGGL(pos_fill_kernel, dim3((int)std::min<int64_t>(ceil_div(n, 256), 8192)), dim3(256), 0, st, p1, n);
+        size_t tb = 0;
+        HIP_CHECK(sort_pairs(nullptr, tb, k1, keys, p1, pos, n, 0, 32, st));
+        void *tmp = arena(ctx, A_SORT, tb);
+        HIP_CHECK(sort_pairs(tmp, tb, k1, keys, p1, pos, n, 0, 32, st));
+        hipLaunchKernelGGL(local_ids_dup_kernel, dim3((int)std::min<int64_t>(ceil_div(n, 256), 8192)), dim3(256), 0, st,
+                           keys, n, err);
+    }
+    hipLaunchKernelGGL(local_ids_kernel, dim3(g), dim3(256), 0, st, keys, pos, n, va, vb, ne, node, fake1, fake2,
+                       node_out, err);
+    int h = 0;
+    HIP_CHECK(hipMemcpyAsync(&h, err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (h & 1) HDB_THROW(HDB_EINVAL, "local MST ids: duplicate vertex ids in the partition");
+    if (h & 2) HDB_THROW(HDB_EINVAL, "local MST ids: an edge vertex is not in the partition");
 }
 
 // ------------------------------------------------------- pairwise distance

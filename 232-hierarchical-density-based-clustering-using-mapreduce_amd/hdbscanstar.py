@@ -165,6 +165,24 @@ class HDBSCANStar:
                                      int(bool(selfEdges)), A.ptr(va), A.ptr(vb), A.ptr(w)), "constructMST")
         return UndirectedGraph(va, vb, w)
 
+    def constructLocalMST(self, dataSet, indices, coreDistances, selfEdges: bool, distanceFunction=None,
+                          node: int = 0):
+        """CreateLocalMST.constructMST (partition/mappers/CreateLocalMST.java:187-292): the
+        reference Prim plus its MinimumSpanningTree record fields -- returns (va, vb, w, fake1,
+        fake2, node) with fake1 = nearestneighborsID (:242), fake2 = otherVertexIndicesID
+        (:266), node (:285); format with formats.format_local_mst (CreateLocalMST.java:110-123)."""
+        g = self.constructMST(dataSet, coreDistances, selfEdges, distanceFunction, indices)
+        va, vb, w = g.getVerticeA(), g.getVericeB(), g.getEges()
+        n = A.Arr(dataSet, np.float64).obj.shape[0]
+        ids = A.Arr(indices, np.int32) if indices is not None else None
+        a, b = A.Arr(va, np.int32), A.Arr(vb, np.int32)
+        ne = a.obj.shape[0]
+        f1, f2, nd = (A.new_like(a, (ne,), np.int32) for _ in range(3))
+        c = _ctx(a, self.ctx)
+        A.check(A.lib().hdb_local_mst_ids(c.h, ids.p if ids else None, n, a.p, b.p, ne, int(node), A.ptr(f1),
+                                          A.ptr(f2), A.ptr(nd)), "hdb_local_mst_ids")
+        return va, vb, w, f1, f2, nd
+
     def constructMSTBoruvka(self, dataSet, coreDistances, selfEdges: bool, distanceFunction=None) -> UndirectedGraph:
         """Large-graph MST (K2b): same sorted weights as constructMST, ties broken by
         (w, min id, max id); edges sorted by that key, then the self edges."""

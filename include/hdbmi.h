@@ -209,6 +209,16 @@ int hdb_copy(hdb_ctx *ctx, void *dst, const void *src, int64_t bytes);
 int hdb_merge_edges(hdb_comm *comm, const int32_t *va, const int32_t *vb, const double *w, const int64_t *seq,
                     int64_t e_local, int32_t **va_all, int32_t **vb_all, double **w_all, int64_t *e_all);
 
+/* CreateLocalMST's record fields (partition/mappers/CreateLocalMST.java:242,266,276-285):
+ * for a partition's edge list with global vertex ids (e.g. hdb_prim_mst / hdb_leaf_msts /
+ * hdb_exact_mst output), fake1[e] / fake2[e] = the local index of va[e] / vb[e] in the
+ * partition's `indices` (ids, n; NULL = identity), node_out[e] = node (nullable).  On
+ * hdb_prim_mst's output this is exactly nearestneighborsID / otherVertexIndicesID, so
+ * hdb_format_mst_records reproduces the reference's local-MST text.  Errors: HDB_EINVAL on
+ * duplicate ids or an edge vertex outside the partition.  Synchronises. */
+int hdb_local_mst_ids(hdb_ctx *ctx, const int32_t *ids, int64_t n, const int32_t *va, const int32_t *vb, int64_t ne,
+                      int32_t node, int32_t *fake1, int32_t *fake2, int32_t *node_out);
+
 /* ------------------------------------------------ global flat labels (§8(f) #1)
  * The step the reference never completes (Main.java:351-408): HDBSCAN* hierarchy over the
  * merged MST and its flat FOSC / excess-of-mass partition -- HDBSCANStar.java:208-625

@@ -173,7 +173,7 @@ static double distance_bubbles(double distance, const double *eB, const double *
 
 static int prim_core(const double *X, int64_t n, int d, const double *core, const int32_t *ids,
                      int metric, int self_edges, const double *eB, const double *nnB, int32_t *va,
-                     int32_t *vb, double *w) {
+                     int32_t *vb, double *w, int32_t *parent_local) {
     if (n < 1 || d <= 0) return ORC_EINVAL;
     unsigned char *attached = (unsigned char *)calloc((size_t)n, 1);
     int32_t *parent = (int32_t *)calloc((size_t)n, sizeof(int32_t));
@@ -198,6 +198,7 @@ static int prim_core(const double *X, int64_t n, int d, const double *core, cons
             if (mrd < best[nb]) {
                 best[nb] = mrd;
                 parent[nb] = ids[cur];
+                if (parent_local) parent_local[nb] = (int32_t)cur; /* CreateLocalMST.java:242 nearestneighborsID */
             }
             if (best[nb] <= nearestD) {
                 nearestD = best[nb];
@@ -230,7 +231,31 @@ static int prim_core(const double *X, int64_t n, int d, const double *core, cons
 
 int orc_prim_mst(const double *X, int64_t n, int d, const double *core, const int32_t *ids, int metric,
                  int self_edges, int32_t *va, int32_t *vb, double *w) {
-    return prim_core(X, n, d, core, ids, metric, self_edges, NULL, NULL, va, vb, w);
+    return prim_core(X, n, d, core, ids, metric, self_edges, NULL, NULL, va, vb, w, NULL);
+}
+
+/* CreateLocalMST.constructMST (partition/mappers/CreateLocalMST.java:187-292): the Prim above
+ * plus the record fields it keeps -- fake1 = nearestneighborsID (the parent's local index,
+ * :242), fake2 = otherVertexIndicesID (the vertex's local index, :266), node (:285); self
+ * edges carry (vertex, vertex, node) (:276-282). */
+int orc_create_local_mst(const double *X, int64_t n, int d, const double *core, const int32_t *ids, int metric,
+                         int self_edges, int32_t node, int32_t *va, int32_t *vb, double *w, int32_t *fake1,
+                         int32_t *fake2, int32_t *node_out) {
+    if (n < 1) return ORC_EINVAL;
+    int32_t *pl = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+    if (!pl) return ORC_ENOMEM;
+    int rc = prim_core(X, n, d, core, ids, metric, self_edges, NULL, NULL, va, vb, w, pl);
+    if (rc == ORC_OK) {
+        const int64_t ne = (n - 1) + (self_edges ? n : 0);
+        for (int64_t i = 0; i < ne; i++) {
+            const int64_t v = i < n - 1 ? i : i - (n - 1);
+            fake1[i] = i < n - 1 ? pl[i] : (int32_t)v;
+            fake2[i] = (int32_t)v;
+            node_out[i] = node;
+        }
+    }
+    free(pl);
+    return rc;
 }
 
 /* ---------------------------------------------------------- nearest sample
@@ -425,7 +450,7 @@ done:
 int orc_bubble_prim_mst(const double *rep, const double *eB, const double *nnB, const int32_t *id_bubbles,
                         const double *core, int64_t b, int d, int metric, int self_edges, int32_t *va,
                         int32_t *vb, double *w) {
-    return prim_core(rep, b, d, core, id_bubbles, metric, self_edges, eB, nnB, va, vb, w);
+    return prim_core(rep, b, d, core, id_bubbles, metric, self_edges, eB, nnB, va, vb, w, NULL);
 }
 
 /* ------------------------------------------------------------- quicksort

@@ -64,6 +64,7 @@ def lib():
         L.orc_quicksort_edges.argtypes = [ip, ip, dp, i64]
         L.orc_merge_edges.argtypes = [ip, ip, dp, i64]
         L.orc_core_rows.argtypes = [dp, i64, i32, lp, i64, i32, i32, i32, dp]
+        L.orc_create_local_mst.argtypes = [dp, i64, i32, dp, ip, i32, i32, i32, ip, ip, dp, ip, ip, ip]
         L.orc_core_rows_par.argtypes = [dp, i64, i32, lp, i64, i32, i32, i32, i32, dp]
         L.orc_prim_mst_par.argtypes = [dp, i64, i32, dp, i32, i32, ip, ip, dp]
         L.orc_local_model.argtypes = [dp, dp, i64, i32, i32, i32, i32, ip, ip, ip, dp, ip, ip, dp, lp]
@@ -166,6 +167,22 @@ def prim_mst(X, core, ids=None, metric="euclidean", self_edges=True):
     _chk(lib().orc_prim_mst(px, n, d, pc, pi, _metric(metric), int(self_edges),
                             _i(va)[1], _i(vb)[1], _d(w)[1]), "prim_mst")
     return va, vb, w
+
+
+def create_local_mst(X, core, ids, node, metric="euclidean", self_edges=True):
+    """CreateLocalMST.constructMST (CreateLocalMST.java:187-292) with its record fields:
+    returns (va, vb, w, fake1, fake2, node) in the reference's edge order."""
+    X, px = _d(X)
+    n, d = X.shape
+    core, pc = _d(core)
+    ids, pi = _i(ids)
+    ne = (n - 1) + (n if self_edges else 0)
+    out = [np.zeros(ne, np.int32), np.zeros(ne, np.int32), np.zeros(ne, np.float64), np.zeros(ne, np.int32),
+           np.zeros(ne, np.int32), np.zeros(ne, np.int32)]
+    _chk(lib().orc_create_local_mst(px, n, d, pc, pi, _metric(metric), int(self_edges), int(node), _i(out[0])[1],
+                                    _i(out[1])[1], _d(out[2])[1], _i(out[3])[1], _i(out[4])[1], _i(out[5])[1]),
+         "create_local_mst")
+    return tuple(out)
 
 
 def nearest_sample(X, S, metric="euclidean", x_key=None, s_key=None):

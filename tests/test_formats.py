@@ -170,3 +170,37 @@ def test_dataset_to_local_mst_text_on_device(pkg, oracle):
     ref_core = oracle.core_distances(X, 4, semantics=oracle.EXCL_SELF)
     _, _, rw = oracle.prim_mst(X, ref_core, self_edges=False)
     assert np.array_equal(np.sort(pw[: X.shape[0] - 1]), np.sort(rw))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["iris", "skin"])
+def test_create_local_mst_text_byte_exact(pkg, oracle, which):
+    """CreateLocalMST end to end on the device: EXCL_SELF cores (CreateLocalMST.java:138-185),
+    reference Prim with global ids, the record fields fake1/fake2/node (hdb_local_mst_ids) and
+    the text (hdb_format_mst_records) equal the oracle's restatement byte for byte."""
+    from conftest import load_iris, load_skin
+    X = load_iris() if which == "iris" else load_skin(2000)
+    n = X.shape[0]
+    rng = np.random.default_rng(7)
+    ids = np.sort(rng.choice(10 * n, size=n, replace=False)).astype(np.int32)  # the subset's global ids
+    node = 37
+    star = pkg.HDBSCANStar()
+    core = star.calculateCoreDistances(X, 4, None, pkg.CORE_EXCL_SELF)
+    got = star.constructLocalMST(X, ids, core, True, None, node)
+    ref = oracle.create_local_mst(X, oracle.core_distances(X, 4, semantics=oracle.EXCL_SELF), ids, node)
+    for g, r in zip(got, ref):
+        assert np.array_equal(np.asarray(g), r)
+    assert pkg.format_local_mst(*got) == OF.format_local_mst(*ref)
+    # the record fields of another edge order (K2b) are the local indices of its vertices
+    va, vb = ref[0][::-1].copy(), ref[1][::-1].copy()
+    f1, f2, nd = (np.zeros(va.shape[0], np.int32) for _ in range(3))
+    ctx = pkg.Context.get(0)
+    A = pkg._capi
+    A.check(A.lib().hdb_local_mst_ids(ctx.h, A.ptr(ids), n, A.ptr(va), A.ptr(vb), va.shape[0], 5, A.ptr(f1),
+                                      A.ptr(f2), A.ptr(nd)), "local ids")
+    assert np.array_equal(ids[f1], va) and np.array_equal(ids[f2], vb) and np.all(nd == 5)
+    bad = va.copy()
+    bad[0] = 10 * n + 1
+    with pytest.raises(pkg.HdbError):
+        A.check(A.lib().hdb_local_mst_ids(ctx.h, A.ptr(ids), n, A.ptr(bad), A.ptr(vb), va.shape[0], 5, A.ptr(f1),
+                                          A.ptr(f2), A.ptr(nd)), "local ids")

@@ -259,3 +259,17 @@ def test_cpu_all_variants_equal_serial(oracle):
             assert np.array_equal(oracle.core_rows_par(X, rows, 4, t), ref)
             pa, pb, pw = oracle.prim_mst_par(X, core, t)
             assert np.array_equal(pa, va) and np.array_equal(pb, vb) and np.array_equal(pw, w)
+
+
+def test_create_local_mst_record_fields(oracle):
+    """CreateLocalMST.java:187-292: the tracked nearestneighborsID / otherVertexIndicesID are
+    the local indices of each record's vertices; the edges are HDBSCANStar's Prim edges."""
+    X = load_iris()
+    core = oracle.core_distances(X, 4, semantics=oracle.EXCL_SELF)
+    ids = (np.arange(X.shape[0], dtype=np.int32) * 7 + 3)
+    va, vb, w, f1, f2, nd = oracle.create_local_mst(X, core, ids, 11)
+    ra, rb, rw = oracle.prim_mst(X, core, ids)
+    assert np.array_equal(va, ra) and np.array_equal(vb, rb) and np.array_equal(w, rw)
+    assert np.array_equal(ids[f1], va) and np.array_equal(ids[f2], vb) and np.all(nd == 11)
+    n = X.shape[0]
+    assert np.array_equal(f2[:n - 1], np.arange(n - 1)) and np.array_equal(f1[n - 1:], np.arange(n))
