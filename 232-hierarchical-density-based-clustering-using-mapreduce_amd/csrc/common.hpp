@@ -70,8 +70,11 @@ struct hdb_ctx {
     int leaf_list_rounds = 2;      // exact leaf: Boruvka rounds seeded from the k-NN lists (A/B: tools/seedk_ab.py)
     bool boruvka_knn_seed = true;  // exact leaf: k-NN lists seed every Boruvka round
     int boruvka_wave_pts = 64;     // points per scan wave (16/32/64), compacted per 512-position group
+    int boruvka_early_pts = 0;     // points per scan wave in rounds < boruvka_early_rounds (0: as above)
+    int boruvka_early_rounds = 5;
     int trav_pop_test = 0;         // bit 0: Boruvka re-tests a popped node, bit 1: K1t a popped leaf
     bool prim_coop = true;         // cooperative single-launch Prim for 4096 < n <= 65536
+    bool prim_coop_slots = true;   // ... with step-tagged slots and the row in registers (d <= 16)
     bool count_evals = false;  // K1t counts evaluated pairs (diagnostic; costs one sync)
     std::map<std::string, int64_t> stats;  // diagnostic counters (count_evals)
 };

@@ -265,6 +265,10 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
         ctx->prim_coop = value != 0;
         return HDB_OK;
     }
+    if (k == "prim_coop_slots") {
+        ctx->prim_coop_slots = value != 0;
+        return HDB_OK;
+    }
     if (k == "leaf_seed_k") {
         if (value < -1 || value > 31) return HDB_EINVAL;
         ctx->leaf_seed_k = (int)value;
@@ -285,6 +289,14 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
     }
     if (k == "boruvka_wave_pts") {
         ctx->boruvka_wave_pts = (int)value;
+        return HDB_OK;
+    }
+    if (k == "boruvka_early_pts") {
+        ctx->boruvka_early_pts = (int)value;
+        return HDB_OK;
+    }
+    if (k == "boruvka_early_rounds") {
+        ctx->boruvka_early_rounds = (int)value;
         return HDB_OK;
     }
     if (k == "boruvka_knn_seed") {

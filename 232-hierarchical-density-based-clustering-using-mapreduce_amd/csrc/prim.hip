@@ -432,6 +432,226 @@ __global__ __launch_bounds__(BS) void prim_coop_kernel(PrimIn in, int n, int sel
     }
 }
 
+// ------------------------------------------ cooperative kernel, step-tagged slots
+// Same Prim (HDBSCANStar.java:124-205, select '<=' = last index, update '<'), restructured
+// around the step's critical path: each lane keeps its own row (d <= DM), core and bubble
+// terms in registers; a workgroup publishes its candidate TOGETHER with that candidate's row
+// in a slot whose tag (the step) is stored last with release semantics; wave 0 of every
+// workgroup polls the nwg tags (acquire), folds the candidates and reads the winner's row
+// (one word per lane) into LDS.  No barrier counter and no dependent load of X[cur].  Slots
+// are double buffered by step parity (a workgroup is at most one step ahead).  (Measured:
+// 6.3 us/step at 16 workgroups vs 7.0 for the counter barrier, 7.2 vs 17.8 at 4; a variant
+// with data-tagged 8-byte granules and no fences polled slower: 9-38 us/step.)
+template <int DM>
+struct CoopSlot {  // written by one thread, read word-wise with agent-scope loads
+    unsigned long long tag, val, idx;
+    double x[DM];
+    double core, eB, nnB;
+};
+
+template <int DM>
+__device__ __forceinline__ double coop_mrd(const PrimIn &in, const double (&xc)[DM], double cc, double ebc, double nnc,
+                                           const double (&xi)[DM], double ci, double ebi, double nni, double best,
+                                           bool &improves) {
+    double dist;
+    if (in.metric == HDB_METRIC_EUCLIDEAN) {  // the rows stay in registers (predicated, same order)
+        double s = sq_diff(xc[0], xi[0]);
+#pragma unroll
+        for (int c = 1; c < DM; c++)
+            if (c < in.d) s = s + sq_diff(xc[c], xi[c]);
+        if (!in.eB) {
+            const double thr = (best * best) * 1.0000000000000009;  // >= best^2 exactly
+            if (s > thr) {
+                improves = false;
+                return best;
+            }
+        }
+        dist = sqrt(s);
+    } else {
+        dist = metric_distance(xc, xi, in.d, in.metric);
+    }
+    if (in.eB) dist = distance_bubbles(dist, ebc, ebi, nnc, nni);
+    double mrd = dist;
+    if (cc > mrd) mrd = cc;
+    if (ci > mrd) mrd = ci;
+    improves = mrd < best;
+    return mrd;
+}
+
+template <int BS, int DM>
+__global__ __launch_bounds__(BS) void prim_coop2_kernel(PrimIn in, int n, int self_edges, int32_t *__restrict__ va,
+                                                        int32_t *__restrict__ vb, double *__restrict__ w,
+                                                        CoopSlot<DM> *__restrict__ slots, int *err) {
+    constexpr int NW = BS / 64;
+    __shared__ double s_v[NW];
+    __shared__ int s_i[NW];
+    __shared__ double s_row[DM + 3];  // the winner's x, core, eB, nnB
+    __shared__ int s_cur;
+    const int nwg = (int)gridDim.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int i = (int)blockIdx.x * BS + tid;
+    double xi[DM], ci = 0, ebi = 0, nni = 0;
+#pragma unroll
+    for (int c = 0; c < DM; c++) xi[c] = (i < n && c < in.d) ? in.X[(int64_t)i * in.d + c] : 0.0;
+    if (i < n) {
+        ci = in.core[i];
+        if (in.eB) {
+            ebi = in.eB[i];
+            nni = in.nnB[i];
+        }
+    }
+    double best = JMAX;
+    int par = 0;
+    bool att = (i >= n) || (i == n - 1);
+    // the start vertex n-1 (HDBSCANStar.java:145-147): its row from memory, once
+    double xc[DM], cc, ebc = 0, nnc = 0;
+#pragma unroll
+    for (int c = 0; c < DM; c++) xc[c] = c < in.d ? in.X[(int64_t)(n - 1) * in.d + c] : 0.0;
+    cc = in.core[n - 1];
+    if (in.eB) {
+        ebc = in.eB[n - 1];
+        nnc = in.nnB[n - 1];
+    }
+    int cur = n - 1;
+    for (int step = 1; step < n; step++) {
+        double lv = INFINITY;
+        int li = -1;
+        if (!att) {
+            bool imp;
+            const double mrd = coop_mrd<DM>(in, xc, cc, ebc, nnc, xi, ci, ebi, nni, best, imp);
+            if (imp) {
+                best = mrd;
+                par = in.ids[cur];
+            }
+            argmin_last(lv, li, best, i);
+        }
+        wave_argmin_last(lv, li);
+        if (lane == 0) {
+            s_v[wid] = lv;
+            s_i[wid] = li;
+        }
+        __syncthreads();
+        double v = s_v[0];
+        int ii = s_i[0];
+#pragma unroll
+        for (int q = 1; q < NW; q++) argmin_last(v, ii, s_v[q], s_i[q]);
+        const int buf = step & 1;
+        CoopSlot<DM> *my = slots + (size_t)buf * nwg + blockIdx.x;
+        if ((ii >= 0) ? (ii == i) : (tid == 0)) {  // the workgroup's candidate row travels with it
+            unsigned long long *wd = (unsigned long long *)my;
+            __hip_atomic_store(&wd[1], (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&wd[2], (unsigned long long)(long long)ii, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int c = 0; c < DM; c++)
+                __hip_atomic_store(&wd[3 + c], (unsigned long long)__double_as_longlong(xi[c]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&wd[3 + DM], (unsigned long long)__double_as_longlong(ci), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&wd[4 + DM], (unsigned long long)__double_as_longlong(ebi), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&wd[5 + DM], (unsigned long long)__double_as_longlong(nni), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&wd[0], (unsigned long long)step, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (wid == 0) {
+            double bv = INFINITY;
+            int bi = -1, bk = -1;
+            for (int k = lane; k < nwg; k += 64) {
+                const unsigned long long *wd = (const unsigned long long *)(slots + (size_t)buf * nwg + k);
+                unsigned spins = 0;
+                while (__hip_atomic_load(&wd[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) !=
+                       (unsigned long long)step) {
+                    if (++spins > (1u << 26)) {  // a co-residency failure must not hang the device
+                        atomicExch(err, 1);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                const double kv = __longlong_as_double(
+                    (long long)__hip_atomic_load(&wd[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                const int ki = (int)(long long)__hip_atomic_load(&wd[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int pi = bi;
+                argmin_last(bv, bi, kv, ki);
+                if (bi != pi) bk = k;
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {  // fold, carrying the winner's slot
+                const double v2 = __shfl_xor(bv, off);
+                const int i2 = __shfl_xor(bi, off), k2 = __shfl_xor(bk, off);
+                const int pi = bi;
+                argmin_last(bv, bi, v2, i2);
+                if (bi != pi) bk = k2;
+            }
+            if (bk >= 0 && lane < DM + 3) {  // the winner's row: one word per lane
+                const unsigned long long *wd = (const unsigned long long *)(slots + (size_t)buf * nwg + bk);
+                s_row[lane] = __longlong_as_double(
+                    (long long)__hip_atomic_load(&wd[3 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            }
+            if (lane == 0) s_cur = bi;
+        }
+        __syncthreads();
+        cur = s_cur;
+        if (cur < 0) break;  // unreachable (an unattached vertex always exists) -- uniform exit
+#pragma unroll
+        for (int c = 0; c < DM; c++) xc[c] = s_row[c];
+        cc = s_row[DM];
+        ebc = s_row[DM + 1];
+        nnc = s_row[DM + 2];
+        if (i == cur) att = true;
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    }
+    if (i < n - 1) {
+        va[i] = par;
+        vb[i] = in.ids[i];
+        w[i] = best;
+    }
+    if (self_edges && i < n) {
+        va[n - 1 + i] = in.ids[i];
+        vb[n - 1 + i] = in.ids[i];
+        w[n - 1 + i] = in.core[i];
+    }
+}
+
+template <int DM>
+static bool launch_coop2(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
+                         int32_t *va, int32_t *vb, double *w) {
+    constexpr int BS = 1024;
+    const int nwg = (int)ceil_div(n, BS);
+    int coop = 0, ncu = 0, per_cu = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device));
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, prim_coop2_kernel<BS, DM>, BS, 0));
+    if (!coop || (int64_t)per_cu * ncu < nwg) return false;
+    const size_t sbytes = (sizeof(CoopSlot<DM>) * 2 * (size_t)nwg + 255) & ~size_t(255);
+    char *base = (char *)arena(ctx, A_WORK3, sbytes + 256);
+    CoopSlot<DM> *slots = (CoopSlot<DM> *)base;
+    int *err = (int *)(base + sbytes);
+    HIP_CHECK(hipMemsetAsync(base, 0, sbytes + 256, ctx->stream));  // tags 0: no step yet
+    PrimIn L = in;
+    L.X = in.X + o * in.d;
+    L.core = in.core + o;
+    L.ids = in.ids + o;
+    if (in.eB) {
+        L.eB = in.eB + o;
+        L.nnB = in.nnB + o;
+    }
+    int nn = (int)n;
+    int32_t *pva = va + eo, *pvb = vb + eo;
+    double *pw = w + eo;
+    void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &slots, &err};
+    {
+        KernelTimer t(ctx, "prim_coop");
+        HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_coop2_kernel<BS, DM>, dim3(nwg), dim3(BS), args, 0,
+                                             ctx->stream));
+    }
+    int h_err = 0;
+    HIP_CHECK(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (h_err) HDB_THROW(HDB_EDEVICE, "prim_coop: slot poll timed out (workgroups not co-resident)");
+    return true;
+}
+
 static bool launch_coop(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
                         int32_t *va, int32_t *vb, double *w) {
     constexpr int BS = 1024;
@@ -502,7 +722,12 @@ void prim_batched_device(hdb_ctx *ctx, const PrimIn &in, const int64_t *h_offs, 
         int64_t n = h_offs[p + 1] - h_offs[p];
         if (n < 0) HDB_THROW(HDB_EINVAL, "offsets must be non-decreasing");
         eoff[p + 1] = eoff[p] + (n > 0 ? (n - 1) + (self_edges ? n : 0) : 0);
-        if (n > 0) cls[block_class(n)].push_back(p);
+        // wide rows (d >= 8): one workgroup re-reads n x d doubles per step through one CU; the
+        // cooperative kernel keeps one row per lane in registers across ceil(n / 1024) CUs
+        // (C3's 4,096-bubble models: 19.6 -> 7.4 us/step)
+        int c = block_class(n);
+        if (c == 3 && in.d >= 8 && in.d <= 16 && ctx->prim_coop && ctx->prim_coop_slots) c = 4;
+        if (n > 0) cls[c].push_back(p);
     }
     size_t off = 0;
     auto carve = [&](size_t bytes) {
@@ -517,7 +742,15 @@ void prim_batched_device(hdb_ctx *ctx, const PrimIn &in, const int64_t *h_offs, 
         std::vector<int32_t> rest;
         for (int32_t p : cls[4]) {
             int64_t n = h_offs[p + 1] - h_offs[p];
-            if (!launch_coop(ctx, in, h_offs[p] - h_offs[0], n, eoff[p], self_edges, va, vb, w)) rest.push_back(p);
+            const int64_t o = h_offs[p] - h_offs[0];
+            bool ok = false;
+            if (n <= 65536 && ctx->prim_coop_slots) {  // step-tagged slots, the row in registers
+                if (in.d <= 4) ok = launch_coop2<4>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                else if (in.d <= 8) ok = launch_coop2<8>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                else if (in.d <= 16) ok = launch_coop2<16>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+            }
+            if (!ok) ok = launch_coop(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+            if (!ok) rest.push_back(p);
         }
         cls[4].swap(rest);
     }

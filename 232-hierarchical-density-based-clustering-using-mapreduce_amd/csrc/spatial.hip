@@ -1578,7 +1578,11 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
     const int64_t ngroups = ceil_div(n, (int64_t)WGRP);
     const int P = ctx->boruvka_wave_pts;
     if (P != 16 && P != 32 && P != 64) HDB_THROW(HDB_EINVAL, "boruvka_wave_pts must be 16, 32 or 64");
-    const int64_t max_waves = ngroups * (WGRP / P);
+    // early rounds search few lanes (few waves in flight for a latency-bound walk): optionally
+    // spread their work over more, smaller waves
+    const int PE = ctx->boruvka_early_pts ? ctx->boruvka_early_pts : P;
+    if (PE != 16 && PE != 32 && PE != 64) HDB_THROW(HDB_EINVAL, "boruvka_early_pts must be 16, 32 or 64");
+    const int64_t max_waves = ngroups * (WGRP / std::min(P, PE));
     int32_t *work = ex.take<int32_t>(per);
     int32_t *gcnt = ex.take<int32_t>(ngroups), *gwaves = ex.take<int32_t>(ngroups), *woff = ex.take<int32_t>(ngroups);
     unsigned long long *desc = ex.take<unsigned long long>(max_waves);
@@ -1661,14 +1665,15 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
         {
             KernelTimer ts(ctx, "boruvka_scan");
             KernelTimer tr(ctx, round_names[round < 8 ? round : 8]);
+            const int Pr = round < ctx->boruvka_early_rounds ? PE : P;
             hipLaunchKernelGGL(group_compact_kernel<D>, dim3((unsigned)ngroups), dim3(WGRP), 0, st, recs, n,
-                               kl ? kl->done : nullptr, bs.lbw, comp_w, P, work, gcnt, gwaves);
+                               kl ? kl->done : nullptr, bs.lbw, comp_w, Pr, work, gcnt, gwaves);
             size_t tb = 0;
             HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, gwaves, woff, (int)ngroups, st));
             void *tmp = arena(ctx, A_SORT, tb);
             HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, gwaves, woff, (int)ngroups, st));
             hipLaunchKernelGGL(wave_desc_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(ngroups, 256), 4096)),
-                               dim3(256), 0, st, gcnt, woff, ngroups, P, desc, nwaves);
+                               dim3(256), 0, st, gcnt, woff, ngroups, Pr, desc, nwaves);
             if (evals)
                 hipLaunchKernelGGL((boruvka_bvh_kernel<D, true>), dim3((unsigned)ceil_div(max_waves, 4)), dim3(256), 0,
                                    st, recs, n, ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, work, desc,

@@ -444,10 +444,40 @@ def test_prim_cooperative_vs_oracle(pkg, oracle, n, kind):
     va, vb, w = oracle.prim_mst(X, core)
     ctx = pkg.Context.get(0)
     star = pkg.HDBSCANStar(ctx)
-    for coop in (1, 0):
+    for coop, slots in ((1, 1), (1, 0), (0, 0)):
         ctx.set_option("prim_coop", coop)
+        ctx.set_option("prim_coop_slots", slots)
         try:
             g = star.constructMST(X, core, True)
         finally:
             ctx.set_option("prim_coop", 1)
-        assert eq(g.getVerticeA(), va) and eq(g.getVericeB(), vb) and eq(g.getEges(), w), coop
+            ctx.set_option("prim_coop_slots", 1)
+        assert eq(g.getVerticeA(), va) and eq(g.getVericeB(), vb) and eq(g.getEges(), w), (coop, slots)
+
+
+@pytest.mark.parametrize("d,metric,n", [(8, "euclidean", 9000), (16, "euclidean", 5000), (5, "cosine", 6000),
+                                        (2, "manhattan", 4500)])
+def test_prim_coop_slots_metrics_and_bubbles(pkg, oracle, d, metric, n):
+    """The step-tagged cooperative Prim (rows in registers, d <= 16) equals the reference
+    Prim for every metric, and the bubble Prim (HdbscanDataBubbles.java:165-254, the C3/C5
+    bubble models it was written for) on > 4096 bubbles."""
+    X = blobs(n, d, 9, n + d, spread=20.0)
+    core = oracle.core_distances(X, 4, metric=metric, semantics=0)
+    ids = (np.arange(n, dtype=np.int32) * 3 + 1)
+    va, vb, w = oracle.prim_mst(X, core, ids, metric=metric)
+    star = pkg.HDBSCANStar(pkg.Context.get(0))
+    dist = {"euclidean": pkg.EuclideanDistance(), "cosine": pkg.CosineSimilarity(),
+            "manhattan": pkg.ManhattanDistance()}[metric]
+    g = star.constructMST(X, core, True, dist, ids)
+    assert eq(g.getVerticeA(), va) and eq(g.getVericeB(), vb) and eq(g.getEges(), w)
+    if metric != "euclidean":
+        return
+    rng = np.random.default_rng(n)
+    eB = np.abs(rng.normal(0.3, 0.1, n))
+    nnB = np.abs(rng.normal(0.2, 0.05, n))
+    nB = rng.integers(1, 9, n).astype(np.int32)
+    bcore = oracle.bubble_core_distances(X, nB, eB, nnB, 4)
+    ra, rb, rw = oracle.bubble_prim_mst(X, eB, nnB, bcore, ids)
+    model = pkg.HdbscanDataBubbles()
+    mst = model.constructMSTBubbles(X, nB, eB, nnB, ids, bcore, True)
+    assert eq(mst.getVerticeA(), ra) and eq(mst.getVericeB(), rb) and eq(mst.getEges(), rw)
