@@ -66,7 +66,7 @@ class MRHDBSCANStar:
     def __init__(self, minPts=4, minClSize=4, processing_units=50, k=0.2, samples_per_subset=None,
                  seed=20210101, distanceFunction=None, all_inter_edges=True, max_levels=64, ctx=None,
                  device=0, flat_labels=True, profile=False, exact_prim_leaves=False, group=None,
-                 prim_leaf_max=LEAF_PRIM_MAX):
+                 prim_leaf_max=LEAF_PRIM_MAX, model_threads=4):
         self.minPts = minPts
         self.minClSize = minClSize
         self.processing_units = processing_units
@@ -88,6 +88,10 @@ class MRHDBSCANStar:
         # leaves up to this size run the reference Prim (exact topology, latency-bound: one
         # step per point); larger ones K2b where it applies (exact weights, ties may differ)
         self.prim_leaf_max = prim_leaf_max
+        # a level's local models run concurrently, one host thread (own context and stream)
+        # each: a bubble Prim occupies only ceil(b / 1024) CUs
+        self.model_threads = model_threads
+        self._pool = None
         self.group = group      # torch.distributed group (None: the default group, if any)
         self._comm = None       # HdbComm for the merge under nccl
         self.timings = {}
@@ -253,25 +257,30 @@ class MRHDBSCANStar:
             # local models: LPT over the ranks on b^2, results gathered, applied in subset order
             nonempty_of = [np.nonzero(info_h[s_off[i]:s_off[i + 1], 2] > 0)[0] for i in range(len(big))]  # D4
             owner = P.lpt([int(ne.shape[0]) ** 2 for ne in nonempty_of], world)
-            results = {}
-            for i, (kk, s0, cnt) in enumerate(big):
-                if owner[i] != rank:
-                    continue
+            def model(i):
                 a, b = s_off[i], s_off[i + 1]
                 nonempty = nonempty_of[i]
-                res = (None, None, None)
-                if nonempty.shape[0] >= 2:
-                    try:
-                        labels, (iva, ivb, iw) = self._local_model(rep_h[a:b][nonempty], info_h[a:b][nonempty])
-                    except A.HdbError as e:  # D10
-                        res = (None, e.code, None)
-                    else:
-                        inter = None
-                        if iw.shape[0]:
-                            gid = s_gid_h[a:b][nonempty].astype(np.int32)
-                            inter = (gid[iva], gid[ivb], iw) if self.all_inter_edges else (iva[:1], ivb[:1], iw[:1])
-                        res = (labels, None, inter)
-                results[i] = res
+                if nonempty.shape[0] < 2:
+                    return None, None, None
+                try:
+                    labels, (iva, ivb, iw) = self._local_model(rep_h[a:b][nonempty], info_h[a:b][nonempty],
+                                                               threaded=True)
+                except A.HdbError as e:  # D10
+                    return None, e.code, None
+                inter = None
+                if iw.shape[0]:
+                    gid = s_gid_h[a:b][nonempty].astype(np.int32)
+                    inter = (gid[iva], gid[ivb], iw) if self.all_inter_edges else (iva[:1], ivb[:1], iw[:1])
+                return labels, None, inter
+
+            mine = [i for i in range(len(big)) if owner[i] == rank]
+            if len(mine) > 1 and self.model_threads > 1:
+                if self._pool is None:
+                    from concurrent.futures import ThreadPoolExecutor
+                    self._pool = ThreadPoolExecutor(self.model_threads)
+                results = dict(zip(mine, self._pool.map(model, mine)))
+            else:
+                results = {i: model(i) for i in mine}
             if world > 1:
                 for part in P.allgather_object(results, self.group):
                     results.update(part)
@@ -344,8 +353,9 @@ class MRHDBSCANStar:
             self._mark("flat_labels")
         return out
 
-    def _local_model(self, rep, info):
-        """LocalModelReduceByKey.java:88-104 body (D4 ids) -> (labels, inter-cluster edges)."""
+    def _local_model(self, rep, info, threaded=False):
+        """LocalModelReduceByKey.java:88-104 body (D4 ids) -> (labels, inter-cluster edges).
+        threaded: this thread's own context (private stream) instead of the driver's."""
         rep = np.ascontiguousarray(rep, np.float64)
         info = np.ascontiguousarray(info, np.float64)
         b, d = rep.shape
@@ -354,7 +364,7 @@ class MRHDBSCANStar:
         mva, mvb, mw = np.zeros(ne, np.int32), np.zeros(ne, np.int32), np.zeros(ne)
         iva, ivb, iw = np.zeros(ne, np.int32), np.zeros(ne, np.int32), np.zeros(ne)
         nic = np.zeros(1, np.int64)
-        c = self._c()
+        c = A.Context.get(self.device) if threaded else self._c()
         A.check(A.lib().hdb_local_model(c.h, A.ptr(rep), A.ptr(info), b, d, self.minPts, self.minClSize, self.metric,
                                         A.ptr(labels), A.ptr(mva), A.ptr(mvb), A.ptr(mw), A.ptr(iva), A.ptr(ivb),
                                         A.ptr(iw), A.ptr(nic)), "LocalModelReduceByKey")
