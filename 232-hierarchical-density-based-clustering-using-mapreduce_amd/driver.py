@@ -146,21 +146,42 @@ class MRHDBSCANStar:
                       for i, (k, _) in enumerate(small)}
         else:
             by_key = {}
+        # large forced leaves (D9) where K2b applies: cumulative cores + exact MST (Boruvka:
+        # exact weights) in one call sharing one spatial index (hdb_exact_mst).  A leaf of
+        # ~1e5 points keeps only part of the chip busy, so several run concurrently, each on a
+        # host thread with its own context and stream.
+        big = [(k, r) for k, r in zip(keys, rows_list) if k not in by_key]
+        jobs = {}
+        for k, r in big:
+            n = r.shape[0]
+            Xl = X.index_select(0, r).contiguous()
+            va = torch.empty(2 * n - 1, dtype=torch.int32, device=X.device)
+            jobs[k] = (r, Xl, va, torch.empty_like(va), torch.empty(2 * n - 1, dtype=torch.float64, device=X.device))
+        if big:
+            torch.cuda.current_stream(X.device).synchronize()  # inputs ready for the other streams
+
+        def leaf(k, threaded):
+            r, Xl, va, vb, w = jobs[k]
+            cc = A.Context.get(self.device) if threaded else c
+            A.check(A.lib().hdb_exact_mst(cc.h, Xl.data_ptr(), r.shape[0], X.shape[1], self.minPts, self.metric,
+                                          A.CORE_INCL_SELF_CUMULATIVE, 1, None, va.data_ptr(), vb.data_ptr(),
+                                          w.data_ptr()), "leaf exact MST")
+            if threaded:
+                cc.synchronize()
+
+        if len(big) > 1 and self.model_threads > 1:
+            if self._pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+                self._pool = ThreadPoolExecutor(self.model_threads)
+            list(self._pool.map(lambda k: leaf(k, True), [k for k, _ in big]))
+        else:
+            for k, _ in big:
+                leaf(k, False)
         for k, r in zip(keys, rows_list):
             if k in by_key:
                 out.append(by_key[k])
                 continue
-            # large forced leaf (D9) where K2b applies: cumulative cores + exact MST (Boruvka:
-            # exact weights) in one call sharing one spatial index (hdb_exact_mst)
-            Xl = X.index_select(0, r).contiguous()
-            n = r.shape[0]
-            ne = 2 * n - 1
-            va = torch.empty(ne, dtype=torch.int32, device=X.device)
-            vb = torch.empty_like(va)
-            w = torch.empty(ne, dtype=torch.float64, device=X.device)
-            A.check(A.lib().hdb_exact_mst(c.h, Xl.data_ptr(), n, X.shape[1], self.minPts, self.metric,
-                                          A.CORE_INCL_SELF_CUMULATIVE, 1, None, va.data_ptr(), vb.data_ptr(),
-                                          w.data_ptr()), "leaf exact MST")
+            r, _, va, vb, w = jobs[k]
             g = r.to(torch.int32)
             out.append((g[va.long()], g[vb.long()], w))
         return out

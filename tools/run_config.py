@@ -27,7 +27,7 @@ elif cfg == "c5":
 else:
     raise SystemExit("c1|c3|c5")
 Xd = torch.from_numpy(X).cuda()
-drv = pkg.MRHDBSCANStar(profile=True, **kw)
+drv = pkg.MRHDBSCANStar(profile=True, prim_leaf_max=4096, model_threads=int(os.environ.get("MODEL_THREADS", "4")), **kw)
 t = time.perf_counter()
 r = drv.run(Xd)
 torch.cuda.synchronize()
