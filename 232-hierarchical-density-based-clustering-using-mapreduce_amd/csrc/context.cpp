@@ -1,4 +1,5 @@
 // context.cpp -- hdb_ctx lifetime, scratch arenas, kernel timing, host/device staging.
+#include <cstdlib>
 #include "common.hpp"
 
 namespace hdb {
@@ -159,6 +160,7 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         hipDeviceProp_t prop;
         HIP_CHECK(hipGetDeviceProperties(&prop, device));
         c->num_cus = prop.multiProcessorCount;
+        if (const char *e = getenv("HDB_PRIM_COOP_SLOTS")) c->prim_coop_slots = atoi(e);  // A/B knob
         *out = c;
         return HDB_OK;
     } catch (const Error &e) {
@@ -266,7 +268,8 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
         return HDB_OK;
     }
     if (k == "prim_coop_slots") {
-        ctx->prim_coop_slots = value != 0;
+        if (value < 0 || value > 5) return HDB_EINVAL;
+        ctx->prim_coop_slots = (int)value;
         return HDB_OK;
     }
     if (k == "leaf_seed_k") {

@@ -53,6 +53,41 @@ __device__ __forceinline__ void wave_argmin_last(double &v, int &i) {
     }
 }
 
+
+// Order-preserving u64 key of a non-negative MRD value (+-0 -> 0): min over keys = min value.
+__device__ __forceinline__ unsigned long long mrd_key(double v) {
+    return v == 0.0 ? 0ull : (unsigned long long)__double_as_longlong(v);
+}
+
+// Wave-wide min of a u64 through DPP moves (quad perms, row shifts, row broadcasts): no LDS
+// round trip per stage, unlike __shfl_xor.  The minimum lands in lane 63 and is broadcast.
+#define HDB_DPP_MIN_STEP(x, CTRL, ROWMASK)                                                                  \
+    do {                                                                                                    \
+        const unsigned lo_ = (unsigned)(x), hi_ = (unsigned)((x) >> 32);                                    \
+        const unsigned lo2_ = (unsigned)__builtin_amdgcn_update_dpp((int)lo_, (int)lo_, CTRL, ROWMASK, 0xf, false); \
+        const unsigned hi2_ = (unsigned)__builtin_amdgcn_update_dpp((int)hi_, (int)hi_, CTRL, ROWMASK, 0xf, false); \
+        const unsigned long long y_ = ((unsigned long long)hi2_ << 32) | lo2_;                              \
+        (x) = y_ < (x) ? y_ : (x);                                                                          \
+    } while (0)
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x) {
+    HDB_DPP_MIN_STEP(x, 0xb1, 0xf);   // quad_perm [1,0,3,2]
+    HDB_DPP_MIN_STEP(x, 0x4e, 0xf);   // quad_perm [2,3,0,1]
+    HDB_DPP_MIN_STEP(x, 0x114, 0xf);  // row_shr:4
+    HDB_DPP_MIN_STEP(x, 0x118, 0xf);  // row_shr:8
+    HDB_DPP_MIN_STEP(x, 0x142, 0xa);  // row_bcast:15
+    HDB_DPP_MIN_STEP(x, 0x143, 0xc);  // row_bcast:31
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)x, 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(x >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// highest lane whose predicate holds (-1: none)
+__device__ __forceinline__ int last_lane(bool p) {
+    const unsigned long long m = __ballot(p);
+    return m ? 63 - __clzll(m) : -1;
+}
+
 // ---------------------------------------------------------- block kernel
 // parts: partition list for this launch (indices into offsets); vertex rows of partition
 // p are [offsets[p], offsets[p+1]).  Edges at eoff[p].
@@ -359,7 +394,7 @@ __global__ __launch_bounds__(BS) void prim_coop_kernel(PrimIn in, int n, int sel
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int i = (int)blockIdx.x * BS + tid;
     double best = JMAX;
-    int par = 0;
+    int par = -1;  // partition-local; ids[] applied once at the end (HDBSCANStar.java:137,172: 0 if never set)
     bool att = (i >= n) || (i == n - 1);
     int cur = n - 1;
     for (int step = 1; step < n; step++) {
@@ -369,7 +404,7 @@ __global__ __launch_bounds__(BS) void prim_coop_kernel(PrimIn in, int n, int sel
             double mrd;
             if (mrd_improves(in, cur, i, best, mrd)) {
                 best = mrd;
-                par = in.ids[cur];
+                par = cur;
             }
             argmin_last(lv, li, best, i);
         }
@@ -421,7 +456,7 @@ __global__ __launch_bounds__(BS) void prim_coop_kernel(PrimIn in, int n, int sel
         if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
     }
     if (i < n - 1) {
-        va[i] = par;
+        va[i] = par >= 0 ? in.ids[par] : 0;
         vb[i] = in.ids[i];
         w[i] = best;
     }
@@ -440,8 +475,22 @@ __global__ __launch_bounds__(BS) void prim_coop_kernel(PrimIn in, int n, int sel
 // workgroup polls the nwg tags (acquire), folds the candidates and reads the winner's row
 // (one word per lane) into LDS.  No barrier counter and no dependent load of X[cur].  Slots
 // are double buffered by step parity (a workgroup is at most one step ahead).  (Measured:
-// 6.3 us/step at 16 workgroups vs 7.0 for the counter barrier, 7.2 vs 17.8 at 4; a variant
-// with data-tagged 8-byte granules and no fences polled slower: 9-38 us/step.)
+// 6.3 us/step at 16 workgroups vs 7.0 for the counter barrier, 7.2 vs 17.8 at 4.)  Variants
+// 2-5 below; 4 is the default (3.0 us/step at 16 workgroups, 3.3 at 4, 3.9 at 64: s_memtime
+// phases showed the __shfl_xor argmin folds, the dependent ids[cur] load and the single-lane
+// slot stores, not the fences, held the slot version at 6.3; tools/coop_prof.py).
+#ifdef HDB_COOP_PROF  // phase timestamps of steps [1024, 1088) of workgroup 0 (tools/coop_prof.py)
+__device__ unsigned long long g_coop_prof[64 * 8];
+#define COOP_T(k)                                                                                              \
+    if (blockIdx.x == 0 && tid == 0 && step >= 1024 && step < 1088) g_coop_prof[(step - 1024) * 8 + (k)] =  \
+        __builtin_amdgcn_s_memtime()
+extern "C" int hdb_debug_coop_prof(unsigned long long *out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_coop_prof), sizeof(g_coop_prof));
+}
+#else
+#define COOP_T(k)
+#endif
+
 template <int DM>
 struct CoopSlot {  // written by one thread, read word-wise with agent-scope loads
     unsigned long long tag, val, idx;
@@ -478,7 +527,7 @@ __device__ __forceinline__ double coop_mrd(const PrimIn &in, const double (&xc)[
     return mrd;
 }
 
-template <int BS, int DM>
+template <int BS, int DM, bool FAST>
 __global__ __launch_bounds__(BS) void prim_coop2_kernel(PrimIn in, int n, int self_edges, int32_t *__restrict__ va,
                                                         int32_t *__restrict__ vb, double *__restrict__ w,
                                                         CoopSlot<DM> *__restrict__ slots, int *err) {
@@ -501,7 +550,7 @@ __global__ __launch_bounds__(BS) void prim_coop2_kernel(PrimIn in, int n, int se
         }
     }
     double best = JMAX;
-    int par = 0;
+    int par = -1;
     bool att = (i >= n) || (i == n - 1);
     // the start vertex n-1 (HDBSCANStar.java:145-147): its row from memory, once
     double xc[DM], cc, ebc = 0, nnc = 0;
@@ -514,6 +563,7 @@ __global__ __launch_bounds__(BS) void prim_coop2_kernel(PrimIn in, int n, int se
     }
     int cur = n - 1;
     for (int step = 1; step < n; step++) {
+        COOP_T(0);
         double lv = INFINITY;
         int li = -1;
         if (!att) {
@@ -521,7 +571,7 @@ __global__ __launch_bounds__(BS) void prim_coop2_kernel(PrimIn in, int n, int se
             const double mrd = coop_mrd<DM>(in, xc, cc, ebc, nnc, xi, ci, ebi, nni, best, imp);
             if (imp) {
                 best = mrd;
-                par = in.ids[cur];
+                par = cur;
             }
             argmin_last(lv, li, best, i);
         }
@@ -531,6 +581,7 @@ __global__ __launch_bounds__(BS) void prim_coop2_kernel(PrimIn in, int n, int se
             s_i[wid] = li;
         }
         __syncthreads();
+        COOP_T(1);
         double v = s_v[0];
         int ii = s_i[0];
 #pragma unroll
@@ -552,22 +603,31 @@ __global__ __launch_bounds__(BS) void prim_coop2_kernel(PrimIn in, int n, int se
                                __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&wd[5 + DM], (unsigned long long)__double_as_longlong(nni), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&wd[0], (unsigned long long)step, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (FAST) {  // sc1 payload drained, then the tag (Guideline 16 R1, no release fence)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&wd[0], (unsigned long long)step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                __hip_atomic_store(&wd[0], (unsigned long long)step, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         if (wid == 0) {
+            COOP_T(2);
             double bv = INFINITY;
             int bi = -1, bk = -1;
+            bool tmo = false;
             for (int k = lane; k < nwg; k += 64) {
                 const unsigned long long *wd = (const unsigned long long *)(slots + (size_t)buf * nwg + k);
                 unsigned spins = 0;
-                while (__hip_atomic_load(&wd[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) !=
+                while (__hip_atomic_load(&wd[0], FAST ? __ATOMIC_RELAXED : __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) !=
                        (unsigned long long)step) {
                     if (++spins > (1u << 26)) {  // a co-residency failure must not hang the device
                         atomicExch(err, 1);
+                        tmo = true;
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
+                if (FAST) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // every payload load is sc1
                 const double kv = __longlong_as_double(
                     (long long)__hip_atomic_load(&wd[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                 const int ki = (int)(long long)__hip_atomic_load(&wd[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -583,14 +643,18 @@ __global__ __launch_bounds__(BS) void prim_coop2_kernel(PrimIn in, int n, int se
                 argmin_last(bv, bi, v2, i2);
                 if (bi != pi) bk = k2;
             }
+            COOP_T(3);
+            if (__any(tmo)) bi = bk = -1;  // timed out: every wave leaves at the next check
             if (bk >= 0 && lane < DM + 3) {  // the winner's row: one word per lane
                 const unsigned long long *wd = (const unsigned long long *)(slots + (size_t)buf * nwg + bk);
                 s_row[lane] = __longlong_as_double(
                     (long long)__hip_atomic_load(&wd[3 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             }
             if (lane == 0) s_cur = bi;
+            COOP_T(4);
         }
         __syncthreads();
+        COOP_T(5);
         cur = s_cur;
         if (cur < 0) break;  // unreachable (an unattached vertex always exists) -- uniform exit
 #pragma unroll
@@ -599,10 +663,168 @@ __global__ __launch_bounds__(BS) void prim_coop2_kernel(PrimIn in, int n, int se
         ebc = s_row[DM + 1];
         nnc = s_row[DM + 2];
         if (i == cur) att = true;
-        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+        if (!FAST && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
     }
     if (i < n - 1) {
-        va[i] = par;
+        va[i] = par >= 0 ? in.ids[par] : 0;
+        vb[i] = in.ids[i];
+        w[i] = best;
+    }
+    if (self_edges && i < n) {
+        va[n - 1 + i] = in.ids[i];
+        vb[n - 1 + i] = in.ids[i];
+        w[n - 1 + i] = in.core[i];
+    }
+}
+
+// Variant (prim_coop_slots = 2): the same exchange as data-tagged 8-byte granules
+// (cdna_hip_programming.md Guideline 16, R2): the candidate's wave stores its payload as
+// {tag = step, 32-bit half} granules, one write-through (sc1) store per lane, no fence; wave 0
+// of every workgroup sweeps all nwg slots flat (granule j on lane j mod 64), staging them in LDS
+// until every tag matches, then folds from LDS.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+template <int BS, int DM>
+__global__ __launch_bounds__(BS) void prim_coop3_kernel(PrimIn in, int n, int self_edges, int32_t *__restrict__ va,
+                                                        int32_t *__restrict__ vb, double *__restrict__ w,
+                                                        gu64 *__restrict__ gr, int *err) {
+    constexpr int NW = BS / 64;
+    constexpr int ND = 1 + DM + 3;  // value, row, core, eB, nnB
+    constexpr int G = 2 * ND + 1;   // + the index
+    constexpr int MAXWG = 64;
+    __shared__ double s_v[NW];
+    __shared__ int s_i[NW];
+    __shared__ unsigned s_g[MAXWG * G];
+    __shared__ double s_row[DM + 3];
+    __shared__ int s_cur;
+    const int nwg = (int)gridDim.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int i = (int)blockIdx.x * BS + tid;
+    double xi[DM], ci = 0, ebi = 0, nni = 0;
+#pragma unroll
+    for (int c = 0; c < DM; c++) xi[c] = (i < n && c < in.d) ? in.X[(int64_t)i * in.d + c] : 0.0;
+    if (i < n) {
+        ci = in.core[i];
+        if (in.eB) {
+            ebi = in.eB[i];
+            nni = in.nnB[i];
+        }
+    }
+    double best = JMAX;
+    int par = -1;
+    bool att = (i >= n) || (i == n - 1);
+    double xc[DM], cc, ebc = 0, nnc = 0;
+#pragma unroll
+    for (int c = 0; c < DM; c++) xc[c] = c < in.d ? in.X[(int64_t)(n - 1) * in.d + c] : 0.0;
+    cc = in.core[n - 1];
+    if (in.eB) {
+        ebc = in.eB[n - 1];
+        nnc = in.nnB[n - 1];
+    }
+    int cur = n - 1;
+    const int T = nwg * G;
+    for (int step = 1; step < n; step++) {
+        double lv = INFINITY;
+        int li = -1;
+        if (!att) {
+            bool imp;
+            const double mrd = coop_mrd<DM>(in, xc, cc, ebc, nnc, xi, ci, ebi, nni, best, imp);
+            if (imp) {
+                best = mrd;
+                par = cur;
+            }
+            argmin_last(lv, li, best, i);
+        }
+        wave_argmin_last(lv, li);
+        if (lane == 0) {
+            s_v[wid] = lv;
+            s_i[wid] = li;
+        }
+        __syncthreads();
+        double v = s_v[0];
+        int ii = s_i[0];
+#pragma unroll
+        for (int q = 1; q < NW; q++) argmin_last(v, ii, s_v[q], s_i[q]);
+        const int buf = step & 1;
+        const unsigned long long tag = (unsigned long long)(unsigned)step << 32;
+        const int loc = ii >= 0 ? ii - (int)blockIdx.x * BS : 0;  // the candidate's thread (empty: wave 0)
+        if (wid == (loc >> 6)) {  // its wave stores the payload, one granule pair per lane
+            const int src = loc & 63;
+            double pay = lane == 0 ? v : 0.0;
+#pragma unroll
+            for (int c = 0; c < DM; c++) {
+                const double t = __shfl(xi[c], src);
+                if (lane == 1 + c) pay = t;
+            }
+            const double t1 = __shfl(ci, src), t2 = __shfl(ebi, src), t3 = __shfl(nni, src);
+            if (lane == 1 + DM) pay = t1;
+            if (lane == 2 + DM) pay = t2;
+            if (lane == 3 + DM) pay = t3;
+            if (ii < 0 && lane > 0) pay = 0.0;
+            gu64 *g = gr + ((size_t)buf * nwg + blockIdx.x) * G;
+            if (lane < ND) {
+                const unsigned long long bits = (unsigned long long)__double_as_longlong(pay);
+                __hip_atomic_store(g + 2 * lane, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(g + 2 * lane + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (lane == ND) {
+                __hip_atomic_store(g + 2 * ND, tag | (unsigned)ii, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (wid == 0) {
+            const gu64 *g = gr + (size_t)buf * nwg * G;
+            unsigned spins = 0;
+            bool tmo = false;
+            while (true) {
+                bool ok = true;
+                for (int j = lane; j < T; j += 64) {
+                    const unsigned long long x = __hip_atomic_load(g + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok &= (x & 0xffffffff00000000ull) == tag;
+                    s_g[j] = (unsigned)x;
+                }
+                if (__all(ok)) break;
+                if (++spins > (1u << 24)) {  // a co-residency failure must not hang the device
+                    if (lane == 0) atomicExch(err, 1);
+                    tmo = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __builtin_amdgcn_wave_barrier();
+            double bv = INFINITY;
+            int bi = -1, bk = -1;
+            if (lane < nwg) {
+                const unsigned *q = s_g + lane * G;
+                bv = __longlong_as_double((long long)(((unsigned long long)q[1] << 32) | q[0]));
+                bi = (int)q[2 * ND];
+                bk = lane;
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                const double v2 = __shfl_xor(bv, off);
+                const int i2 = __shfl_xor(bi, off), k2 = __shfl_xor(bk, off);
+                const int pi = bi;
+                argmin_last(bv, bi, v2, i2);
+                if (bi != pi) bk = k2;
+            }
+            if (tmo) bi = bk = -1;
+            if (bk >= 0 && lane < DM + 3) {
+                const unsigned *q = s_g + bk * G + 2 * (1 + lane);
+                s_row[lane] = __longlong_as_double((long long)(((unsigned long long)q[1] << 32) | q[0]));
+            }
+            if (lane == 0) s_cur = bi;
+        }
+        __syncthreads();
+        cur = s_cur;
+        if (cur < 0) break;
+#pragma unroll
+        for (int c = 0; c < DM; c++) xc[c] = s_row[c];
+        cc = s_row[DM];
+        ebc = s_row[DM + 1];
+        nnc = s_row[DM + 2];
+        if (i == cur) att = true;
+    }
+    if (i < n - 1) {
+        va[i] = par >= 0 ? in.ids[par] : 0;
         vb[i] = in.ids[i];
         w[i] = best;
     }
@@ -614,6 +836,262 @@ __global__ __launch_bounds__(BS) void prim_coop2_kernel(PrimIn in, int n, int se
 }
 
 template <int DM>
+static bool launch_coop3(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
+                         int32_t *va, int32_t *vb, double *w) {
+    constexpr int BS = 1024;
+    const int nwg = (int)ceil_div(n, BS);
+    if (nwg > 64) return false;
+    int coop = 0, ncu = 0, per_cu = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device));
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, prim_coop3_kernel<BS, DM>, BS, 0));
+    if (!coop || (int64_t)per_cu * ncu < nwg) return false;
+    constexpr int G = 2 * (1 + DM + 3) + 1;
+    const size_t gbytes = (8 * (size_t)G * 2 * nwg + 255) & ~size_t(255);
+    char *base = (char *)arena(ctx, A_WORK3, gbytes + 256);
+    gu64 *gr = (gu64 *)base;
+    int *err = (int *)(base + gbytes);
+    HIP_CHECK(hipMemsetAsync(base, 0, gbytes + 256, ctx->stream));  // tags 0: no step yet
+    PrimIn L = in;
+    L.X = in.X + o * in.d;
+    L.core = in.core + o;
+    L.ids = in.ids + o;
+    if (in.eB) {
+        L.eB = in.eB + o;
+        L.nnB = in.nnB + o;
+    }
+    int nn = (int)n;
+    int32_t *pva = va + eo, *pvb = vb + eo;
+    double *pw = w + eo;
+    void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &gr, &err};
+    {
+        KernelTimer t(ctx, "prim_coop");
+        HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_coop3_kernel<BS, DM>, dim3(nwg), dim3(BS), args, 0,
+                                             ctx->stream));
+    }
+    int h_err = 0;
+    HIP_CHECK(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (h_err) HDB_THROW(HDB_EDEVICE, "prim_coop: granule sweep timed out (workgroups not co-resident)");
+    return true;
+}
+
+// Variant (prim_coop_slots = 4): one step = DPP wave minimum of order-preserving keys (the
+// highest lane among equal keys is the argmin_last winner: indices grow with the lane), the
+// wave's winner lane parks its row in LDS, ONE barrier, wave 0 folds the 16 waves the same way
+// and publishes the workgroup's candidate as data-tagged 8-byte granules (Guideline 16 R2: 3
+// key granules {value lo, value hi, index} + 2 (DM + 3) row granules, one sc1 store per lane),
+// sweeps the nwg x 3 key granules flat until every tag is this step, picks the winner workgroup
+// and reads its row granules straight into the LDS row; ONE barrier.  No fences, no counters.
+template <int BS, int DM, bool FULL>
+__global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int self_edges, int32_t *__restrict__ va,
+                                                        int32_t *__restrict__ vb, double *__restrict__ w,
+                                                        gu64 *__restrict__ gkey, gu64 *__restrict__ grow, int *err) {
+    constexpr int NW = BS / 64;
+    constexpr int ND = DM + 3;  // x, core, eB, nnB
+    __shared__ double s_cand[NW][ND + 1];
+    __shared__ int s_ci[NW];
+    constexpr int G = 3 + 2 * ND;  // FULL: one slot of key + row granules per workgroup
+    __shared__ unsigned s_key[FULL ? G * 64 : 3 * 64];
+    __shared__ double s_row[ND];
+    __shared__ int s_cur;
+    const int nwg = (int)gridDim.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int i = (int)blockIdx.x * BS + tid;
+    double xi[DM], ci = 0, ebi = 0, nni = 0;
+#pragma unroll
+    for (int c = 0; c < DM; c++) xi[c] = (i < n && c < in.d) ? in.X[(int64_t)i * in.d + c] : 0.0;
+    if (i < n) {
+        ci = in.core[i];
+        if (in.eB) {
+            ebi = in.eB[i];
+            nni = in.nnB[i];
+        }
+    }
+    double best = JMAX;
+    int par = -1;
+    bool att = (i >= n) || (i == n - 1);
+    double xc[DM], cc, ebc = 0, nnc = 0;
+#pragma unroll
+    for (int c = 0; c < DM; c++) xc[c] = c < in.d ? in.X[(int64_t)(n - 1) * in.d + c] : 0.0;
+    cc = in.core[n - 1];
+    if (in.eB) {
+        ebc = in.eB[n - 1];
+        nnc = in.nnB[n - 1];
+    }
+    int cur = n - 1;
+    constexpr unsigned long long KINF = 0x7ff0000000000000ull;  // key of +inf: nothing to offer
+    for (int step = 1; step < n; step++) {
+        COOP_T(0);
+        unsigned long long key = KINF;
+        if (!att) {
+            bool imp;
+            const double mrd = coop_mrd<DM>(in, xc, cc, ebc, nnc, xi, ci, ebi, nni, best, imp);
+            if (imp) {
+                best = mrd;
+                par = cur;
+            }
+            key = mrd_key(best);
+        }
+        const unsigned long long wmin = wave_min_u64(key);
+        const int wl = last_lane(key == wmin);
+        if (lane == wl) {  // the wave's candidate parks its row
+#pragma unroll
+            for (int c = 0; c < DM; c++) s_cand[wid][c] = xi[c];
+            s_cand[wid][DM] = ci;
+            s_cand[wid][DM + 1] = ebi;
+            s_cand[wid][DM + 2] = nni;
+            s_cand[wid][ND] = best;
+            s_ci[wid] = wmin < KINF ? i : -1;
+        }
+        __syncthreads();
+        COOP_T(1);
+        if (wid == 0) {
+            const int buf = step & 1;
+            const unsigned tag = (unsigned)step;
+            // fold the waves: lane q holds wave q's candidate
+            const int qi = lane < NW ? s_ci[lane] : -1;
+            const unsigned long long qk = qi >= 0 ? mrd_key(s_cand[lane < NW ? lane : 0][ND]) : KINF;
+            const unsigned long long gmin = wave_min_u64(qk);
+            const int q = min(last_lane(qk == gmin), NW - 1);  // all waves empty: any wave (index -1)
+            const unsigned *cw = (const unsigned *)s_cand[q];
+            const int gidx = __shfl(qi, q);
+            // publish: lanes 0-2 the key granules, lanes 3 .. 3 + 2 ND the row granules
+            unsigned val;
+            if (lane < 2) val = cw[2 * ND + lane];
+            else if (lane == 2) val = (unsigned)gidx;
+            else val = lane < 3 + 2 * ND ? cw[lane - 3] : 0u;
+            const unsigned long long gv = ((unsigned long long)tag << 32) | val;
+            if (FULL) {
+                if (lane < G)
+                    __hip_atomic_store(gkey + ((size_t)buf * nwg + blockIdx.x) * G + lane, gv, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            } else if (lane < 3)
+                __hip_atomic_store(gkey + ((size_t)buf * nwg + blockIdx.x) * 3 + lane, gv, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            else if (lane < 3 + 2 * ND)
+                __hip_atomic_store(grow + ((size_t)buf * nwg + blockIdx.x) * (2 * ND) + (lane - 3), gv, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            COOP_T(2);
+            // sweep every workgroup's key granules
+            constexpr int KS = FULL ? G : 3;  // granules per workgroup in the sweep
+            const gu64 *kb = gkey + (size_t)buf * nwg * KS;
+            const int T = KS * nwg;
+            bool tmo = false;
+            for (unsigned spins = 0;;) {
+                bool ok = true;
+                for (int j = lane; j < T; j += 64) {
+                    const unsigned long long x = __hip_atomic_load(kb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok &= (unsigned)(x >> 32) == tag;
+                    s_key[j] = (unsigned)x;
+                }
+                if (__all(ok)) break;
+                if (++spins > (1u << 24)) {  // a co-residency failure must not hang the device
+                    if (lane == 0) atomicExch(err, 1);
+                    tmo = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            COOP_T(3);
+            __builtin_amdgcn_wave_barrier();
+            int kidx = -1;
+            unsigned long long kk = KINF;
+            if (lane < nwg) {
+                kidx = (int)s_key[KS * lane + 2];
+                const double kv = __longlong_as_double(
+                    (long long)(((unsigned long long)s_key[KS * lane + 1] << 32) | s_key[KS * lane]));
+                if (kidx >= 0) kk = mrd_key(kv);
+            }
+            const unsigned long long amin = wave_min_u64(kk);
+            const int k = last_lane(kk == amin);
+            const int win = __shfl(kidx, k);
+            if (tmo || amin == KINF) {
+                if (lane == 0) s_cur = -1;
+            } else {
+                if (FULL) {  // the winner's row is already in LDS
+                    if (lane < 2 * ND) ((unsigned *)s_row)[lane] = s_key[KS * k + 3 + lane];
+                } else if (lane < 2 * ND) {  // the winner's row granules, straight into the LDS row
+                    const gu64 *rb = grow + ((size_t)buf * nwg + k) * (2 * ND) + lane;
+                    unsigned long long x;
+                    for (unsigned spins = 0;;) {
+                        x = __hip_atomic_load(rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((unsigned)(x >> 32) == tag || ++spins > (1u << 24)) break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    ((unsigned *)s_row)[lane] = (unsigned)x;
+                }
+                if (lane == 0) s_cur = win;
+            }
+            COOP_T(4);
+        }
+        __syncthreads();
+        COOP_T(5);
+        cur = s_cur;
+        if (cur < 0) break;
+#pragma unroll
+        for (int c = 0; c < DM; c++) xc[c] = s_row[c];
+        cc = s_row[DM];
+        ebc = s_row[DM + 1];
+        nnc = s_row[DM + 2];
+        if (i == cur) att = true;
+    }
+    if (i < n - 1) {
+        va[i] = par >= 0 ? in.ids[par] : 0;
+        vb[i] = in.ids[i];
+        w[i] = best;
+    }
+    if (self_edges && i < n) {
+        va[n - 1 + i] = in.ids[i];
+        vb[n - 1 + i] = in.ids[i];
+        w[n - 1 + i] = in.core[i];
+    }
+}
+
+template <int DM, bool FULL>
+static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
+                         int32_t *va, int32_t *vb, double *w) {
+    constexpr int BS = 1024;
+    const int nwg = (int)ceil_div(n, BS);
+    if (nwg > 64) return false;
+    int coop = 0, ncu = 0, per_cu = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device));
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, prim_coop4_kernel<BS, DM, FULL>, BS, 0));
+    if (!coop || (int64_t)per_cu * ncu < nwg) return false;
+    constexpr int ND = DM + 3;
+    const size_t kbytes = (8 * (size_t)(FULL ? 3 + 2 * ND : 3) * 2 * nwg + 255) & ~size_t(255);
+    const size_t rbytes = (8 * (size_t)2 * ND * 2 * nwg + 255) & ~size_t(255);
+    char *base = (char *)arena(ctx, A_WORK3, kbytes + rbytes + 256);
+    gu64 *gkey = (gu64 *)base;
+    gu64 *grow = (gu64 *)(base + kbytes);
+    int *err = (int *)(base + kbytes + rbytes);
+    HIP_CHECK(hipMemsetAsync(base, 0, kbytes + rbytes + 256, ctx->stream));  // tags 0: no step yet
+    PrimIn L = in;
+    L.X = in.X + o * in.d;
+    L.core = in.core + o;
+    L.ids = in.ids + o;
+    if (in.eB) {
+        L.eB = in.eB + o;
+        L.nnB = in.nnB + o;
+    }
+    int nn = (int)n;
+    int32_t *pva = va + eo, *pvb = vb + eo;
+    double *pw = w + eo;
+    void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &gkey, &grow, &err};
+    {
+        KernelTimer t(ctx, "prim_coop");
+        HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_coop4_kernel<BS, DM, FULL>, dim3(nwg), dim3(BS), args, 0,
+                                             ctx->stream));
+    }
+    int h_err = 0;
+    HIP_CHECK(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (h_err) HDB_THROW(HDB_EDEVICE, "prim_coop: key sweep timed out (workgroups not co-resident)");
+    return true;
+}
+
+template <int DM, bool FAST>
 static bool launch_coop2(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
                          int32_t *va, int32_t *vb, double *w) {
     constexpr int BS = 1024;
@@ -621,7 +1099,7 @@ static bool launch_coop2(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
     int coop = 0, ncu = 0, per_cu = 0;
     HIP_CHECK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device));
     HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, prim_coop2_kernel<BS, DM>, BS, 0));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, prim_coop2_kernel<BS, DM, FAST>, BS, 0));
     if (!coop || (int64_t)per_cu * ncu < nwg) return false;
     const size_t sbytes = (sizeof(CoopSlot<DM>) * 2 * (size_t)nwg + 255) & ~size_t(255);
     char *base = (char *)arena(ctx, A_WORK3, sbytes + 256);
@@ -642,7 +1120,7 @@ static bool launch_coop2(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
     void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &slots, &err};
     {
         KernelTimer t(ctx, "prim_coop");
-        HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_coop2_kernel<BS, DM>, dim3(nwg), dim3(BS), args, 0,
+        HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_coop2_kernel<BS, DM, FAST>, dim3(nwg), dim3(BS), args, 0,
                                              ctx->stream));
     }
     int h_err = 0;
@@ -744,10 +1222,31 @@ void prim_batched_device(hdb_ctx *ctx, const PrimIn &in, const int64_t *h_offs, 
             int64_t n = h_offs[p + 1] - h_offs[p];
             const int64_t o = h_offs[p] - h_offs[0];
             bool ok = false;
-            if (n <= 65536 && ctx->prim_coop_slots) {  // step-tagged slots, the row in registers
-                if (in.d <= 4) ok = launch_coop2<4>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
-                else if (in.d <= 8) ok = launch_coop2<8>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
-                else if (in.d <= 16) ok = launch_coop2<16>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+            if (n <= 65536 && ctx->prim_coop_slots == 4) {  // DPP folds + key/row granules
+                if (in.d <= 4) ok = launch_coop4<4, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                else if (in.d <= 8) ok = launch_coop4<8, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                else if (in.d <= 16) ok = launch_coop4<16, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+            }
+            if (n <= 65536 && ctx->prim_coop_slots == 5) {  // ... every candidate row in the sweep
+                if (in.d <= 4) ok = launch_coop4<4, true>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                else if (in.d <= 8) ok = launch_coop4<8, true>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                else if (in.d <= 16) ok = launch_coop4<16, true>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+            }
+            if (!ok && n <= 65536 && ctx->prim_coop_slots == 2) {  // data-tagged granules
+                if (in.d <= 4) ok = launch_coop3<4>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                else if (in.d <= 8) ok = launch_coop3<8>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                else if (in.d <= 16) ok = launch_coop3<16>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+            }
+            if (!ok && n <= 65536 && ctx->prim_coop_slots) {  // step-tagged slots, the row in registers
+                if (ctx->prim_coop_slots == 3) {  // write-through payload + drained tag, relaxed poll
+                    if (in.d <= 4) ok = launch_coop2<4, true>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                    else if (in.d <= 8) ok = launch_coop2<8, true>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                    else if (in.d <= 16) ok = launch_coop2<16, true>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                } else {
+                    if (in.d <= 4) ok = launch_coop2<4, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                    else if (in.d <= 8) ok = launch_coop2<8, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                    else if (in.d <= 16) ok = launch_coop2<16, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                }
             }
             if (!ok) ok = launch_coop(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
             if (!ok) rest.push_back(p);

@@ -35,6 +35,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import numpy as np
 
 from . import _capi as A
@@ -90,12 +92,13 @@ class MRHDBSCANStar:
         self.prim_leaf_max = prim_leaf_max
         # a level's local models run concurrently, one host thread (own context and stream)
         # each: a bubble Prim occupies only ceil(b / 1024) CUs
-        self.model_threads = model_threads
+        self.model_threads = int(os.environ.get("HDB_MODEL_THREADS", model_threads))
         self._pool = None
         self.group = group      # torch.distributed group (None: the default group, if any)
         self._comm = None       # HdbComm for the merge under nccl
         self.timings = {}
         self._t0 = None
+        self._progress = bool(os.environ.get("HDB_PROGRESS"))  # one stderr line per level
 
     def _mark(self, phase):
         if not self.profile:
@@ -198,6 +201,8 @@ class MRHDBSCANStar:
         self.timings = {}
         self._t0 = None
         self._mark(None)
+        import time
+        t_run = time.perf_counter()
         world, rank = P.world_rank(self.group)
         key_of = torch.zeros(n, dtype=torch.int64, device=dev)
         alive = torch.arange(n, dtype=torch.int64, device=dev)  # ids in the current _unprocessed_ file
@@ -237,6 +242,14 @@ class MRHDBSCANStar:
                 for kk, r in zip(leaf_k, leaf_rows):
                     leaf_of[r] = kk
             iteration += 1
+            if self._progress:
+                import sys
+                import time
+                print(f"[hdb] level {iteration - 1}: {len(leaf_k)} leaves, {len(big)} big subsets, "
+                      f"{processed}/{n} points done, {time.perf_counter() - t_run:.2f} s", file=sys.stderr, flush=True)
+                if os.environ.get("HDB_WATCHDOG"):  # every thread's stack if a level stalls
+                    import faulthandler
+                    faulthandler.dump_traceback_later(float(os.environ["HDB_WATCHDOG"]), exit=False)
             if processed >= n:
                 levels.append(level)
                 break
@@ -286,7 +299,9 @@ class MRHDBSCANStar:
                 try:
                     labels, (iva, ivb, iw) = self._local_model(rep_h[a:b][nonempty], info_h[a:b][nonempty],
                                                                threaded=True)
-                except A.HdbError as e:  # D10
+                except A.HdbError as e:  # D10: the reference's own exceptions only
+                    if e.code > -10:
+                        raise
                     return None, e.code, None
                 inter = None
                 if iw.shape[0]:

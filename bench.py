@@ -147,6 +147,10 @@ def run_partitioned(args, workload):
                             samples_per_subset=cfg["samples_per_subset"], prim_leaf_max=4096, profile=args.phases)
     out = {}
 
+    if os.environ.get("HDB_WATCHDOG"):  # diagnosis: every thread's Python stack every N s
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["HDB_WATCHDOG"]))  # re-armed per level
+
     def job():
         Xd = X_pin.to("cuda", non_blocking=True)
         r = drv.run(Xd)

@@ -444,14 +444,14 @@ def test_prim_cooperative_vs_oracle(pkg, oracle, n, kind):
     va, vb, w = oracle.prim_mst(X, core)
     ctx = pkg.Context.get(0)
     star = pkg.HDBSCANStar(ctx)
-    for coop, slots in ((1, 1), (1, 0), (0, 0)):
+    for coop, slots in ((1, 5), (1, 4), (1, 3), (1, 2), (1, 1), (1, 0), (0, 0)):
         ctx.set_option("prim_coop", coop)
         ctx.set_option("prim_coop_slots", slots)
         try:
             g = star.constructMST(X, core, True)
         finally:
             ctx.set_option("prim_coop", 1)
-            ctx.set_option("prim_coop_slots", 1)
+            ctx.set_option("prim_coop_slots", 4)
         assert eq(g.getVerticeA(), va) and eq(g.getVericeB(), vb) and eq(g.getEges(), w), (coop, slots)
 
 

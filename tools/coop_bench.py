@@ -23,7 +23,7 @@ ids = torch.arange(n, dtype=torch.int32).cuda()
 ctx = pkg.Context.get(0)
 ctx.use_torch_stream()
 star, model = pkg.HDBSCANStar(ctx), pkg.HdbscanDataBubbles(ctx)
-for slots in (1, 0):
+for slots in (5, 4, 1):
     ctx.set_option("prim_coop_slots", slots)
     for name, f in (("prim", lambda: star.constructMST(X, core, True, None, ids)),
                     ("bubble_prim", lambda: model.constructMSTBubbles(X, nB, eB, nnB, ids, core, True))):
@@ -35,4 +35,4 @@ for slots in (1, 0):
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t) / 3
         print(f"slots={slots} {name:12s} n={n} d={d}: {dt * 1e3:8.2f} ms  ({dt / n * 1e6:.2f} us/step)")
-ctx.set_option("prim_coop_slots", 1)
+ctx.set_option("prim_coop_slots", 4)
