@@ -114,6 +114,90 @@ def cpu_baseline(X, budget_s=10.0):
                                         f"(x{(n / m_1) ** 2:.0f}); extrapolated full step {tot_1:.0f} s"}}
 
 
+C4 = dict(n=2_000_000, d=128, centers=200, noise=0.1, seed=4, min_pts=16)
+MFMA_BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
+
+
+def run_c4(args):
+    """BASELINE config 4: 2M x 128 L2-normalised embeddings, core distances over minPts = 16
+    (EXCL_SELF) on the MFMA path (K1m: bf16-split norm-expansion screen on MFMA + exact FP64
+    re-check of every pair the screen cannot exclude; lists bit-identical to the FP64 scan).
+    Timed region: pinned host X -> H2D -> core distances -> D2H of the cores.  One GPU (the
+    core distances of one partition; C4 names no sharding).  Roofline: the algorithmic
+    2 n^2 d flops of all-pairs dot products / the K1m kernel time vs the dense bf16 peak."""
+    import torch
+    pkg = importlib.import_module(PKG)
+    A = importlib.import_module(PKG + "._capi")
+    n = args.n if args.n != N_POINTS else C4["n"]
+    d, mp = C4["d"], C4["min_pts"]
+    g = torch.Generator(device="cuda").manual_seed(C4["seed"])
+    C = torch.randn(C4["centers"], d, dtype=torch.float64, device="cuda", generator=g)
+    lab = torch.randint(0, C4["centers"], (n,), device="cuda", generator=g)
+    X = C[lab] + C4["noise"] * torch.randn(n, d, dtype=torch.float64, device="cuda", generator=g)
+    X_pin = (X / torch.linalg.norm(X, dim=1, keepdim=True)).cpu().pin_memory()
+    del X, C, lab
+    ctx = pkg.Context.get(0)
+    ctx.use_torch_stream()
+    core_h = torch.empty(n, dtype=torch.float64).pin_memory()
+
+    def step():
+        Xd = X_pin.to("cuda", non_blocking=True)
+        core = torch.empty(n, dtype=torch.float64, device="cuda")
+        A.check(A.lib().hdb_core_distances(ctx.h, Xd.data_ptr(), n, d, mp, A.METRIC["euclidean"], A.CORE_EXCL_SELF,
+                                           core.data_ptr()), "core distances")
+        core_h.copy_(core, non_blocking=True)
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    ctx.kernel_time("knn_mfma")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    k_ms, k_calls = ctx.kernel_time("knn_mfma")
+    ctx.set_timing(False)
+    k_s = k_ms / 1e3 / args.steps  # K1m kernel time of one step (HIP events on its stream)
+    n_pad = -(-n // 64) * 64
+    alg = 2.0 * n * n * d
+    issued = 2 * 3 * 2.0 * n_pad * n_pad * d  # bound + exact pass, 3 bf16 products each (split operands)
+    c = core_h.numpy()
+    assert np.all(np.isfinite(c)) and np.all(c >= 0)
+    line = {"metric": "points/sec end-to-end + mutual-reach distance evals/sec at 1/2/4/8 GPUs",
+            "value": n / dt, "unit": "points/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64 (bf16-split MFMA screen + f64 re-check)",
+            "data": f"synthetic (L2-normalised embeddings, {C4['centers']} centers + N(0, {C4['noise']}^2), seed {C4['seed']})",
+            "config": {"workload": "config 4: 2M x 128 embeddings, core distances minPts 16 (EXCL_SELF) on the MFMA path",
+                       "points": n, "d": d, "min_pts": mp,
+                       "timed": "pinned host X -> H2D -> K1m core distances -> D2H of the cores"},
+            "mrd_evals_per_s": n * (n - 1) / dt,
+            "roofline": {"bound": "mfma", "kernel": "knn_mfma (K1m)", "achieved": alg / k_s / 1e12,
+                         "peak": MFMA_BF16_DENSE_TFLOPS, "unit": "TFLOP/s", "frac": alg / k_s / 1e12 / MFMA_BF16_DENSE_TFLOPS,
+                         "traffic": None, "work": "algorithmic 2 n^2 d (all-pairs dot products)",
+                         "issued_mfma_tflops": issued / k_s / 1e12, "kernel_s_per_step": k_s,
+                         "launches_per_step": k_calls / args.steps}}
+    if not args.no_cpu_baseline:
+        from oracle import oracle as O
+        O.lib()
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        Xh = X_pin.numpy()
+        rows = np.linspace(0, n - 1, 16 * threads).astype(np.int64)
+        t0 = time.perf_counter()
+        O.core_rows_par(Xh, rows, mp, threads)
+        t_r = time.perf_counter() - t0
+        full = t_r * n / rows.shape[0]
+        line["cpu_baseline"] = {"value": n / full, "unit": "points/s", "cores": threads, "kind": "port",
+                                "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+                                "sample": f"oracle C -O2, OpenMP {threads} threads: core distances of {rows.shape[0]} "
+                                          f"query rows vs all {n} rows (x{n / rows.shape[0]:.0f}); "
+                                          f"extrapolated full step {full:.0f} s"}
+    print(json.dumps(line), flush=True)
+
+
 PARTITIONED = {  # SURVEY.md §8(d) C3 / C5 (recursive sampling, data bubbles), strong scaling
     "c3": dict(n=4_000_000, d=16, centers=50, spread=50.0, seed=3, samples_per_subset=4096, processing_units=65536,
                desc="config 3: blobs 4M x 16, recursive sampling (4,096 samples/subset, pu 65,536)"),
@@ -203,15 +287,21 @@ def run_partitioned(args, workload):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="default 10 (c2), 1 (c3/c4/c5)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 3 (c2), 0 (c3/c5), 1 (c4)")
     ap.add_argument("--n", type=int, default=N_POINTS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["c2", "c3", "c5"], default="c2",
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2 (default): the per-GPU C2 pipeline (weak scaling); c3/c5: the whole "
                          "partitioned job over the sharded driver (strong scaling)")
     ap.add_argument("--phases", action="store_true", help="c3/c5: per-phase times (synchronising)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 10 if args.workload == "c2" else 1
+    if args.warmup is None:
+        args.warmup = {"c2": 3, "c4": 1}.get(args.workload, 0)
+    if args.workload == "c4":
+        return run_c4(args)
     if args.workload != "c2":
         return run_partitioned(args, args.workload)
 

@@ -109,3 +109,20 @@ def test_mfma_rechecks_few(ctx, star):
         star.knn(X, 15, None, exclSelf=True)
         re = ctx.get_stat("knn_mfma_rechecks")
     assert 0 < re < 0.05 * 20000 ** 2
+
+
+def test_mfma_lists_equal_fp64_200k_x_128(pkg, ctx, star):
+    """C4's shape at 200k rows (BASELINE config 4: 2M x 128 embeddings, minPts 16): the MFMA
+    screen + FP64 re-check must return the same 15-NN lists, bit for bit, as the all-pairs FP64
+    scan (K1) over all 200k x 200k pairs.  Data generated on the device (seeded)."""
+    import torch
+    n, d, k = 200_000, 128, 15
+    g = torch.Generator(device="cuda").manual_seed(44)
+    C = torch.randn(200, d, dtype=torch.float64, device="cuda", generator=g)
+    lab = torch.randint(0, 200, (n,), device="cuda", generator=g)
+    X = C[lab] + 0.1 * torch.randn(n, d, dtype=torch.float64, device="cuda", generator=g)
+    X = (X / torch.linalg.norm(X, dim=1, keepdim=True)).contiguous()
+    got = lists(ctx, star, X, k, True)
+    ref = lists(ctx, star, X, k, False)
+    assert got.shape == (n, k)
+    assert torch.equal(got.view(torch.int64), ref.view(torch.int64))
