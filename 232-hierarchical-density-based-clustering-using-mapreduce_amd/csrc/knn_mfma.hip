@@ -32,6 +32,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
+#include <vector>
 
 #include "internal.hpp"
 
@@ -320,14 +322,347 @@ __global__ __launch_bounds__(NT) void knn_mfma_kernel(const double *__restrict__
     }
 }
 
+// ---------------------------------------------------------------- single pass (default)
+// K1m-s: ONE MFMA pass over all pairs (the two-pass kernel above is the fallback).  Per
+// query it keeps the KC smallest rigorous UPPER bounds (approx + bound, FP32 rounded up) of
+// the candidates seen so far: their largest, thr, is >= the KC-th smallest exact value T*.
+// Every candidate whose LOWER bound (approx - bound) is <= the running thr is appended to the
+// query's candidate log (id, lower bound rounded down).  thr only decreases, so a candidate
+// left out of the log has lb > thr_at_that_time >= thr_final >= T*: its exact value exceeds
+// T* and it cannot be among the KC smallest.  A second, tiny kernel re-computes the logged
+// candidates with lb <= thr_final in exact FP64 (the reference's order) and keeps the KC
+// smallest -- the lists equal the FP64 scan bit for bit.  The deferred re-check takes the
+// FP64 work (and its random row loads) out of the MFMA loop; the pass is not repeated.
+//
+// Tiles: candidates are the MFMA A operand (rows), queries the B operand (columns), so a lane
+// holds one query per 32 x 32 tile and its screen constants are per-lane scalars.  A wave
+// keeps QT query tiles resident in VGPRs (bf16 hi/lo fragments); the four waves of a
+// workgroup share each 32-candidate block, staged global -> LDS by global_load_lds (16 B,
+// XOR-swizzled 16-B chunks: conflict-free ds_read_b128), double-buffered, one barrier per
+// block.  The screen per pair is one FMA, one subtract and one max: with
+//     g = eps |q| / 2,  hc = c2 (1 - 4e-6) / 2,  a = (q2 (1 - 4e-6) - thr) / 2
+// a pair can pass the FP64 test  (q2 + c2 - 2 acc) - bound <= thr  only if
+//     fma(g, |c|, acc) - hc >= a
+// (the 4e-6 (q2 + c2) margin covers every FP32 rounding of this test); a wave branches to
+// the rare hit path only when a lane's maximum over its 16 pairs reaches a.
+constexpr int S_LOGCAP = 512;  // log entries per query (compacted against thr when full)
+struct LogEnt {
+    int cid;
+    float lb;
+};
+constexpr int S_CST = 192;  // per 32-candidate block: hc[32], cn[32] (float), c2[32], cn[32] (double)
+
+#ifndef HDB_K1S_WAVES
+#define HDB_K1S_WAVES 4  // waves per workgroup (A/B knob: 8 = one workgroup of 512 queries per CU)
+#endif
+constexpr int NW = HDB_K1S_WAVES;
+template <int DP>
+struct ScreenCfg {
+    static constexpr int QT = DP <= 128 ? 2 : 1;  // query tiles per wave (VGPR-resident fragments)
+    static constexpr int SQ = NW * 32 * QT;       // queries per workgroup
+    static constexpr int CH = DP / 8;             // 16-B chunks per bf16 row
+    static constexpr int BUF = 2 * 32 * DP;       // bf16 elements per staged block (hi rows, lo rows)
+};
+
+__device__ __forceinline__ float f32_down(double x) {
+    float f = (float)x;
+    if ((double)f > x) f = nextafterf(f, -INFINITY);
+    return f;
+}
+__device__ __forceinline__ float f32_up(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = nextafterf(f, INFINITY);
+    return f;
+}
+
+// per-block screen constants, packed so one global_load_lds stages them
+__global__ void screen_consts_kernel(const double *__restrict__ nrm2, const double *__restrict__ nrm, int64_t n_pad,
+                                     float *__restrict__ cst) {
+    HDB_GRID_STRIDE(r, n_pad) {
+        float *b = cst + (r >> 5) * S_CST;
+        const int i = (int)(r & 31);
+        b[i] = (float)(nrm2[r] * (1.0 - 4e-6) * 0.5);
+        b[32 + i] = (float)nrm[r];
+        ((double *)(b + 64))[i] = nrm2[r];
+        ((double *)(b + 128))[i] = nrm[r];
+    }
+}
+
+// the log of one query is full: keep the entries that can still matter (lb <= thr)
+__device__ __noinline__ int log_compact(LogEnt *L, float t) {
+    int w = 0;
+    for (int j = 0; j < S_LOGCAP; j++) {
+        const LogEnt e = L[j];
+        if (e.lb <= t) L[w++] = e;
+    }
+    return w;
+}
+
+typedef __attribute__((address_space(3))) void *lds_ptr_t;
+
+template <int DP, int KC>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void knn_mfma_screen_kernel(
+    const __bf16 *__restrict__ Xh, const __bf16 *__restrict__ Xl, const double *__restrict__ nrm2,
+    const double *__restrict__ nrm, const float *__restrict__ cst, int64_t n, int64_t n_pad, int excl,
+    LogEnt *__restrict__ logs, int *__restrict__ log_cnt, float *__restrict__ thr_out, int *__restrict__ overflow) {
+    using C = ScreenCfg<DP>;
+    constexpr int QT = C::QT, SQ = C::SQ, CH = C::CH, BUF = C::BUF, NS = DP / KS;
+    // two distinct LDS objects per double buffer: the compiler's waitcnt pass then knows the
+    // LDS-DMA into one buffer does not alias reads of the other (no vmcnt(0) before them)
+    __shared__ __attribute__((aligned(16))) __bf16 cb0_s[BUF];
+    __shared__ __attribute__((aligned(16))) __bf16 cb1_s[BUF];
+    __shared__ __attribute__((aligned(16))) float cst0_s[S_CST];
+    __shared__ __attribute__((aligned(16))) float cst1_s[S_CST];
+    auto cbuf = [&](auto B) -> __bf16 * {
+        if constexpr (decltype(B)::value == 0) return cb0_s;
+        else return cb1_s;
+    };
+    auto cstb = [&](auto B) -> float * {
+        if constexpr (decltype(B)::value == 0) return cst0_s;
+        else return cst1_s;
+    };
+    __shared__ float top_s[SQ * KC];
+    __shared__ int cnt_s[SQ];
+    __shared__ double qn2_s[SQ], qn_s[SQ];
+
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, half = lane >> 5, col = lane & 31;
+    const int64_t qbase = (int64_t)blockIdx.x * SQ;
+    const double eps_dot = 2.0 * (3.1 * 0x1p-16 + 3.0 * DP * 0x1p-24) * 1.01;
+    const float epsf = (float)eps_dot * 1.001f;
+    const bool ex = excl != 0;
+
+    for (int i = tid; i < SQ * KC; i += 64 * NW) top_s[i] = INFINITY;
+    for (int i = tid; i < SQ; i += 64 * NW) {
+        cnt_s[i] = 0;
+        qn2_s[i] = nrm2[qbase + i];
+        qn_s[i] = nrm[qbase + i];
+    }
+    bf16x8 bh[QT][NS], bl[QT][NS];
+    float g[QT], qh[QT], a[QT];
+    int qloc[QT];
+#pragma unroll
+    for (int t = 0; t < QT; t++) {
+        qloc[t] = wave * 32 * QT + 32 * t + col;
+        const int64_t row = qbase + qloc[t];
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            const int64_t o = row * DP + KS * s + 8 * half;
+            bh[t][s] = *(const bf16x8 *)(Xh + o);
+            bl[t][s] = *(const bf16x8 *)(Xl + o);
+        }
+        g[t] = epsf * (float)nrm[row] * 0.5f;
+        qh[t] = (float)(nrm2[row] * (1.0 - 4e-6) * 0.5);
+        a[t] = -INFINITY;
+    }
+
+    // global -> LDS staging of one 32-candidate block (all of it is LDS-DMA: nothing else is
+    // in flight on the vector-memory counter when the barrier drains it).  CH wave-
+    // instructions per block (CH/2 per array), CH/NW per wave; each lane's source offset inside
+    // the block is fixed (swizzle on the source address, the LDS image stays lane-linear).
+    constexpr int GW = (CH + NW - 1) / NW;  // wave-instructions per wave per block
+    uint32_t goff[GW];
+#pragma unroll
+    for (int k = 0; k < GW; k++) {
+        const int i = (wave + NW * k) % CH, ii = i >= CH / 2 ? i - CH / 2 : i;
+        const int p = ii * 64 + lane, row = p / CH, pc = p % CH, lc = pc ^ (row & (CH - 1));
+        goff[k] = (uint32_t)(row * DP + lc * 8);
+    }
+    auto stage = [&](auto B, int64_t cb) {
+        __bf16 *base = cbuf(B);
+#pragma unroll
+        for (int k = 0; k < GW; k++) {
+            const int i = wave + NW * k;
+            if (CH % NW != 0 && i >= CH) break;  // wave-uniform
+            const int arr = i >= CH / 2, ii = arr ? i - CH / 2 : i;
+            const __bf16 *src = (arr ? Xl : Xh) + cb * DP;  // uniform
+            __builtin_amdgcn_global_load_lds((const void *)(src + goff[k]),
+                                             (lds_ptr_t)(base + arr * 32 * DP + ii * 512), 16, 0, 0);
+        }
+        if (wave == 0 && lane < S_CST / 4)
+            __builtin_amdgcn_global_load_lds((const void *)(cst + (cb >> 5) * S_CST + lane * 4),
+                                             (lds_ptr_t)cstb(B), 16, 0, 0);
+    };
+
+    const int64_t nblk = n_pad / 32;  // even (n_pad is a multiple of 512)
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    auto step = [&](auto B, auto Bn, int64_t blk) {
+        const int64_t cb = blk * 32;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // block blk landed everywhere; block blk-1's buffer is free
+        if (blk + 1 < nblk) stage(Bn, cb + 32);
+        float *const cst_s = cstb(B);
+
+        const __bf16 *hb = cbuf(B), *lb = hb + 32 * DP;
+        f32x16 acc[QT];
+#pragma unroll
+        for (int t = 0; t < QT; t++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[t][r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            const int pc = (2 * s + half) ^ (col & (CH - 1));
+            const bf16x8 ah = *(const bf16x8 *)(hb + col * DP + pc * 8);
+            const bf16x8 al = *(const bf16x8 *)(lb + col * DP + pc * 8);
+#pragma unroll
+            for (int t = 0; t < QT; t++) {
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[t][s], acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[t][s], acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t][s], acc[t], 0, 0, 0);
+            }
+        }
+        // screen: C row (candidate) = 8 gi + 4 half + u, column (query) = col
+        const float4 *hc4 = (const float4 *)cst_s, *cn4 = (const float4 *)(cst_s + 32);
+        float m[QT];
+#pragma unroll
+        for (int t = 0; t < QT; t++) m[t] = -INFINITY;
+#pragma unroll
+        for (int gi = 0; gi < 4; gi++) {
+            const float4 h4 = hc4[2 * gi + half], c4 = cn4[2 * gi + half];
+#pragma unroll
+            for (int t = 0; t < QT; t++) {
+                m[t] = fmaxf(m[t], fmaf(g[t], c4.x, acc[t][4 * gi + 0]) - h4.x);
+                m[t] = fmaxf(m[t], fmaf(g[t], c4.y, acc[t][4 * gi + 1]) - h4.y);
+                m[t] = fmaxf(m[t], fmaf(g[t], c4.z, acc[t][4 * gi + 2]) - h4.z);
+                m[t] = fmaxf(m[t], fmaf(g[t], c4.w, acc[t][4 * gi + 3]) - h4.w);
+            }
+        }
+        bool hit = false;
+#pragma unroll
+        for (int t = 0; t < QT; t++) hit |= m[t] >= a[t];
+        if (__ballot(hit)) {
+            // rare: the two half-waves hold the same queries, so they take turns
+            const double *c2d = (const double *)(cst_s + 64), *cnd = (const double *)(cst_s + 128);
+            for (int h = 0; h < 2; h++) {
+                if (half == h) {
+#pragma unroll
+                    for (int t = 0; t < QT; t++) {
+                        const int ql = qloc[t];
+                        const int64_t qid = qbase + ql;
+                        if (!(m[t] >= a[t]) || qid >= n) continue;
+                        const double q2 = qn2_s[ql], qn = qn_s[ql];
+                        float *tp = top_s + ql * KC;
+#pragma unroll 1
+                        for (int r = 0; r < 16; r++) {
+                            const int ci = 8 * (r >> 2) + 4 * half + (r & 3);
+                            const float av = acc[t][r];  // dynamic element (rare path)
+                            const float v = fmaf(g[t], cst_s[32 + ci], av) - cst_s[ci];
+                            const int64_t cid = cb + ci;
+                            if (!(v >= a[t]) || cid >= n || (ex && cid == qid)) continue;
+                            const double c2 = c2d[ci], cn = cnd[ci];
+                            const double approx = (q2 + c2) - 2.0 * (double)av;
+                            const double bound = eps_dot * qn * cn + 4e-13 * (q2 + c2) + 1e-30;
+                            const double lbv = approx - bound;
+                            const float thr = tp[KC - 1];
+                            if (!(lbv <= (double)thr)) continue;
+                            int k = cnt_s[ql];
+                            if (k == S_LOGCAP) {
+                                k = log_compact(logs + qid * S_LOGCAP, thr);
+                                if (k == S_LOGCAP) {
+                                    atomicAdd(overflow, 1);
+                                    k = S_LOGCAP + 1;  // this query's lists are not trusted
+                                }
+                                cnt_s[ql] = k;
+                            }
+                            if (k < S_LOGCAP) {
+                                LogEnt e;
+                                e.cid = (int)cid;
+                                e.lb = f32_down(lbv);
+                                logs[qid * S_LOGCAP + k] = e;
+                                cnt_s[ql] = k + 1;
+                            }
+                            const float ub = f32_up(approx + bound);
+                            if (ub < thr) {
+                                int i = KC - 1;
+                                for (; i > 0 && tp[i - 1] > ub; i--) tp[i] = tp[i - 1];
+                                tp[i] = ub;
+                            }
+                        }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+#pragma unroll
+            for (int t = 0; t < QT; t++) a[t] = qh[t] - 0.5f * top_s[qloc[t] * KC + KC - 1];
+        }
+    };
+    stage(B0{}, 0);
+    for (int64_t blk = 0; blk < nblk; blk += 2) {
+        step(B0{}, B1{}, blk);
+        step(B1{}, B0{}, blk + 1);
+    }
+    __syncthreads();
+    for (int i = tid; i < SQ; i += 64 * NW) {
+        const int64_t qid = qbase + i;
+        if (qid < n) {
+            log_cnt[qid] = cnt_s[i] > S_LOGCAP ? -1 : cnt_s[i];
+            thr_out[qid] = top_s[i * KC + KC - 1];
+        }
+    }
+}
+
+// exact FP64 re-check of each query's logged candidates with lb <= thr (one wave per query),
+// then the KC smallest over the wave: the same values, in the same order, as the FP64 scan
+template <int KC>
+__global__ __launch_bounds__(256) void knn_mfma_final_kernel(const double *__restrict__ X, int64_t n, int d,
+                                                             const LogEnt *__restrict__ logs,
+                                                             const int *__restrict__ log_cnt,
+                                                             const float *__restrict__ thr,
+                                                             double *__restrict__ lists) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (q >= n) return;
+    const int cnt = log_cnt[q];
+    const float t = thr[q];
+    double top[KC];
+#pragma unroll
+    for (int k = 0; k < KC; k++) top[k] = INFINITY;
+    for (int j = lane; j < cnt; j += 64) {
+        const LogEnt e = logs[q * S_LOGCAP + j];
+        if (e.lb <= t) topk_insert<KC>(top, exact_sq<0>(X + q * d, X + (int64_t)e.cid * d, d));
+    }
+    for (int k = 0; k < KC; k++) {
+        double mn = top[0];
+        for (int o = 32; o >= 1; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
+        const unsigned long long b = __ballot(top[0] == mn);
+        if (lane == __ffsll((long long)b) - 1) {
+#pragma unroll
+            for (int i = 0; i + 1 < KC; i++) top[i] = top[i + 1];
+            top[KC - 1] = INFINITY;
+        }
+        if (lane == 0) lists[q * KC + k] = (mn < INFINITY) ? sqrt(mn) : JMAX;
+    }
+}
+
 // ---------------------------------------------------------------- host
+template <int DP, int KC>
+static void launch_single(hdb_ctx *ctx, const double *X, int64_t n, int64_t n_pad, int d, const __bf16 *Xh,
+                          const __bf16 *Xl, const double *nrm2, const double *nrm, const float *cst, int excl,
+                          LogEnt *logs, int *log_cnt, float *thr, int *overflow, double *lists) {
+    hipStream_t st = ctx->stream;
+    using C = ScreenCfg<DP>;
+    {
+        KernelTimer t(ctx, "knn_mfma");
+        hipLaunchKernelGGL((knn_mfma_screen_kernel<DP, KC>), dim3((unsigned)(n_pad / C::SQ)), dim3(64 * NW), 0, st, Xh,
+                           Xl, nrm2, nrm, cst, n, n_pad, excl, logs, log_cnt, thr, overflow);
+        HIP_CHECK(hipGetLastError());
+    }
+    {
+        KernelTimer t(ctx, "knn_mfma_final");
+        hipLaunchKernelGGL((knn_mfma_final_kernel<KC>), dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, X, n, d,
+                           logs, log_cnt, thr, lists);
+        HIP_CHECK(hipGetLastError());
+    }
+}
+
 template <int DP>
 static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC, bool excl, double *lists) {
-    const int64_t n_pad = ceil_div(n, (int64_t)MQ) * MQ;
+    const int64_t n_pad = ceil_div(n, (int64_t)512) * 512;  // multiple of MQ and of every SQ
     const int nb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, n / 64));
     auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
     const size_t bytes = 2 * rnd(sizeof(__bf16) * (size_t)(n_pad * DP)) + 3 * rnd(8 * (size_t)n_pad) +
-                         2 * rnd(8 * (size_t)nb * d) + rnd(8 * (size_t)d) + 256 + 256;
+                         2 * rnd(8 * (size_t)nb * d) + rnd(8 * (size_t)d) + 256 + 256 +
+                         rnd(4 * (size_t)(n_pad / 32) * S_CST) + 2 * rnd(4 * (size_t)n_pad);
     char *base = (char *)arena(ctx, A_WORK3, bytes);
     size_t off = 0;
     auto take = [&](size_t b) {
@@ -341,9 +676,11 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
     double *psum = (double *)take(8 * (size_t)nb * d), *pmax = (double *)take(8 * (size_t)nb * d);
     double *mu = (double *)take(8 * (size_t)d);
     double *thr = (double *)take(8 * (size_t)n_pad);
-    const bool two_pass = ctx->knn_mfma_two_pass;
     double *prm = (double *)take(256);
     unsigned long long *stats = (unsigned long long *)take(256);
+    float *cst = (float *)take(4 * (size_t)(n_pad / 32) * S_CST);
+    int *log_cnt = (int *)take(4 * (size_t)n_pad);
+    float *thr_f = (float *)take(4 * (size_t)n_pad);
     hipStream_t st = ctx->stream;
     hipLaunchKernelGGL(col_stats_kernel, dim3(nb), dim3(256), 0, st, X, n, d, nb, psum, pmax);
     hipLaunchKernelGGL(centre_kernel, dim3(1), dim3(256), 0, st, psum, pmax, nb, n, d, mu, prm);
@@ -356,6 +693,43 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
         hipLaunchKernelGGL(split_rows_kernel, dim3(g), dim3(256), 0, st, X, n, n_pad, d, DP, mu, prm, Xh, Xl, nrm2,
                            nrm);
     }
+    if (ctx->knn_mfma_single) {
+        const int g = (int)std::min<int64_t>(ceil_div(n_pad, 256), 4096);
+        hipLaunchKernelGGL(screen_consts_kernel, dim3(g), dim3(256), 0, st, nrm2, nrm, n_pad, cst);
+        LogEnt *logs = (LogEnt *)arena(ctx, A_LOG, sizeof(LogEnt) * (size_t)n_pad * S_LOGCAP);
+        int *overflow = (int *)stats;
+        HIP_CHECK(hipMemsetAsync(overflow, 0, 4, st));
+        const int fl = excl ? 1 : 0;
+#define K1S_CASE(KK)                                                                                              \
+    case KK:                                                                                                      \
+        launch_single<DP, KK>(ctx, X, n, n_pad, d, Xh, Xl, nrm2, nrm, cst, fl, logs, log_cnt, thr_f, overflow, \
+                              lists);                                                                             \
+        break;
+        switch (KC) {
+            K1S_CASE(1)
+            K1S_CASE(3)
+            K1S_CASE(7)
+            K1S_CASE(15)
+            K1S_CASE(31)
+        default: return false;
+        }
+#undef K1S_CASE
+        int h_ovf = 0;
+        HIP_CHECK(hipMemcpyAsync(&h_ovf, overflow, 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        if (ctx->count_evals) {
+            // diagnostic: logged candidates (the FP64 re-checks are those with lb <= thr)
+            std::vector<int> hc((size_t)n);
+            HIP_CHECK(hipMemcpy(hc.data(), log_cnt, 4 * (size_t)n, hipMemcpyDeviceToHost));
+            int64_t tot = 0;
+            for (int v : hc) tot += v < 0 ? S_LOGCAP : v;
+            ctx->stats["knn_mfma_rechecks"] = tot;
+            ctx->stats["last_evals"] = tot;
+        }
+        ctx->stats["knn_mfma_log_overflow"] = h_ovf;
+        if (h_ovf == 0) return true;
+        // a query's log overflowed (e.g. hundreds of exact duplicates): two-pass kernel for all
+    }
     if (ctx->count_evals) HIP_CHECK(hipMemsetAsync(stats, 0, 8, st));
     {
         KernelTimer t(ctx, "knn_mfma");
@@ -363,12 +737,10 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
         const int fl = (excl ? 1 : 0) | (getenv("HDBMI_K1M_DBG") ? 2 : 0);
 #define K1M_CASE(KK)                                                                                             \
     case KK:                                                                                                     \
-        if (two_pass)                                                                                            \
-            hipLaunchKernelGGL((knn_mfma_kernel<DP, KK, 0>), grid, dim3(NT), 0, st, X, n, n_pad, d, Xh, Xl, nrm2, \
-                               nrm, prm, fl, nullptr, thr, lists, nullptr);                                     \
+        hipLaunchKernelGGL((knn_mfma_kernel<DP, KK, 0>), grid, dim3(NT), 0, st, X, n, n_pad, d, Xh, Xl, nrm2,     \
+                           nrm, prm, fl, nullptr, thr, lists, nullptr);                                         \
         hipLaunchKernelGGL((knn_mfma_kernel<DP, KK, 1>), grid, dim3(NT), 0, st, X, n, n_pad, d, Xh, Xl, nrm2,     \
-                           nrm, prm, fl, two_pass ? thr : nullptr, nullptr, lists,                               \
-                           ctx->count_evals ? stats : nullptr);                                                  \
+                           nrm, prm, fl, thr, nullptr, lists, ctx->count_evals ? stats : nullptr);              \
         break;
         switch (KC) {
             K1M_CASE(1)

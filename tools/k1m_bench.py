@@ -24,25 +24,34 @@ X = X / torch.linalg.norm(X, dim=1, keepdim=True)
 X = X.contiguous()
 ctx = pkg.Context.get(0)
 ctx.use_torch_stream()
+SINGLE = int(os.environ.get("K1M_SINGLE", "1"))
+ctx.set_option("knn_mfma_single", SINGLE)
 star = pkg.HDBSCANStar(ctx)
 k = MIN_PTS - 1
 star.knn(X[:4096].contiguous(), k, None, exclSelf=True)  # warm
 torch.cuda.synchronize()
 ctx.set_timing(True)
 ctx.kernel_time("knn_mfma")
+ctx.kernel_time("knn_mfma_final")
 t0 = time.perf_counter()
 L = star.knn(X, k, None, exclSelf=True)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 ms, _ = ctx.kernel_time("knn_mfma")
+ms_final, _ = ctx.kernel_time("knn_mfma_final")
+ovf = ctx.get_stat("knn_mfma_log_overflow") if SINGLE else 0
 ctx.set_timing(False)
+if os.environ.get("K1M_QUICK"):
+    print(json.dumps({"n": n, "d": d, "lib": os.environ.get("HDBMI_LIB", "default"), "wall_s": dt, "knn_mfma_ms": ms,
+                      "knn_mfma_final_ms": ms_final}))
+    sys.exit(0)
 ctx.set_option("count_evals", 1)
 star.knn(X[: min(n, 200_000)].contiguous(), k, None, exclSelf=True)
 re_sub = ctx.get_stat("knn_mfma_rechecks")
 ctx.set_option("count_evals", 0)
-n_pad = -(-n // 64) * 64
+n_pad = -(-n // 256) * 256
 DP = 32 if d <= 32 else 64 if d <= 64 else 128 if d <= 128 else 256
-passes = 2  # upper-bound pass + exact pass (knn_mfma_two_pass)
+passes = 1 if SINGLE else 2  # single pass (screen + log) or upper-bound pass + exact pass
 flops = passes * 3 * 2.0 * n_pad * n_pad * DP  # bf16 split: 3 MFMA products per pass
 # exact spot check (Java order): 16 sampled rows
 rows = torch.randint(0, n, (16,), device="cuda", generator=g)
@@ -55,6 +64,7 @@ for r in rows.tolist():
     s[r] = float("inf")
     ref = torch.sqrt(torch.topk(s, k, largest=False).values)
     bad += int(not torch.equal(ref, L[r]))
-print(json.dumps({"n": n, "d": d, "k": k, "wall_s": dt, "knn_mfma_ms": ms, "mfma_tflops": flops / (ms / 1e3) / 1e12,
-                  "mfma_peak_tflops": 2500.0, "rechecks_per_query_200k": re_sub / min(n, 200_000),
+print(json.dumps({"n": n, "d": d, "k": k, "single": SINGLE, "wall_s": dt, "knn_mfma_ms": ms,
+                  "knn_mfma_final_ms": ms_final, "log_overflow": ovf, "mfma_tflops": flops / (ms / 1e3) / 1e12,
+                  "mfma_peak_tflops": 2500.0, "logged_per_query_200k" if SINGLE else "rechecks_per_query_200k": re_sub / min(n, 200_000),
                   "spot_rows": 16, "spot_mismatch": bad}))

@@ -28,7 +28,7 @@ def load(d):
 
 def main(out):
     res = {}
-    for sub in ("fetch", "write", "sq"):
+    for sub in ("fetch", "write", "sq", "lds"):
         for k, cs in load(os.path.join(out, sub)).items():
             r = res.setdefault(k, {})
             for c, v in cs.items():
