@@ -54,7 +54,7 @@ struct hdb_ctx {
     std::vector<hdb::TimedLaunch> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, std::pair<double, int64_t>> acc;
-    hdb::Arena arenas[12];
+    hdb::Arena arenas[14];
     int64_t *pinned = nullptr;  // pinned_words(): async device -> host counters
     void *host_stage = nullptr;  // host_arena(): grow-only pinned staging
     size_t host_stage_bytes = 0;
@@ -66,6 +66,7 @@ struct hdb_ctx {
     int64_t knn_mfma_min_n = 2048;
     bool knn_mfma_two_pass = true;  // K1m two-pass kernel (fallback): upper-bound pass first (few exact re-checks)
     bool knn_mfma_single = true;    // K1m single pass: screen + candidate log, FP64 re-check of the log
+    bool knn_mfma_prune = true;     // K1m single pass: random-projection order + FP64-ball superblock pruning
     bool boruvka_seed = true;      // seed Boruvka rounds from the previous round's edges
     int leaf_seed_k = -1;          // exact leaf: k-NN list length at least this (-1: by dimension)
     int leaf_list_rounds = 2;      // exact leaf: Boruvka rounds seeded from the k-NN lists (A/B: tools/seedk_ab.py)
@@ -86,7 +87,7 @@ namespace hdb {
 // scratch slot ids
 enum {
     A_STAGE_IN = 0, A_STAGE_OUT = 1, A_WORK0 = 2, A_WORK1 = 3, A_WORK2 = 4, A_WORK3 = 5, A_PAD = 6, A_SORT = 7,
-    A_FLAT0 = 8, A_FLAT1 = 9, A_FLAT_TMP = 10, A_LOG = 11
+    A_FLAT0 = 8, A_FLAT1 = 9, A_FLAT_TMP = 10, A_LOG = 11, A_ORDER = 12
 };
 
 void *arena(hdb_ctx *ctx, int slot, size_t bytes);

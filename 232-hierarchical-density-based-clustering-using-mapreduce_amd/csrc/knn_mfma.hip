@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "internal.hpp"
+#include "sort.hpp"
 
 namespace hdb {
 
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const double *__restric
                                                          int DP, const double *__restrict__ mu,
                                                          const double *__restrict__ prm, __bf16 *__restrict__ Xh,
                                                          __bf16 *__restrict__ Xl, double *__restrict__ nrm2,
-                                                         double *__restrict__ nrm) {
+                                                         double *__restrict__ nrm, const int *__restrict__ perm) {
     const double sc = prm[1];
     // one wave per row
     const int lane = threadIdx.x & 63;
@@ -115,7 +116,8 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const double *__restric
         double acc = 0;
         for (int c = lane; c < DP; c += 64) {
             double v = 0;
-            if (r < n && c < d) v = (X[r * d + c] - mu[c]) * sc;
+            const int64_t src = perm ? (int64_t)perm[r] : (r < n ? r : -1);  // -1: padding row
+            if (src >= 0 && c < d) v = (X[src * d + c] - mu[c]) * sc;
             const __bf16 h = to_bf16(v);
             const __bf16 l = to_bf16(v - (double)(float)h);
             Xh[r * DP + c] = h;
@@ -377,11 +379,12 @@ __device__ __forceinline__ float f32_up(double x) {
 
 // per-block screen constants, packed so one global_load_lds stages them
 __global__ void screen_consts_kernel(const double *__restrict__ nrm2, const double *__restrict__ nrm, int64_t n_pad,
-                                     float *__restrict__ cst) {
+                                     const int *__restrict__ perm, float *__restrict__ cst) {
     HDB_GRID_STRIDE(r, n_pad) {
         float *b = cst + (r >> 5) * S_CST;
         const int i = (int)(r & 31);
-        b[i] = (float)(nrm2[r] * (1.0 - 4e-6) * 0.5);
+        // a padding row of the layout never passes the screen (hc = +inf)
+        b[i] = perm[r] < 0 ? INFINITY : (float)(nrm2[r] * (1.0 - 4e-6) * 0.5);
         b[32 + i] = (float)nrm[r];
         ((double *)(b + 64))[i] = nrm2[r];
         ((double *)(b + 128))[i] = nrm[r];
@@ -398,13 +401,194 @@ __device__ __noinline__ int log_compact(LogEnt *L, float t) {
     return w;
 }
 
+// ---------------------------------------------------------------- candidate order (pruned K1m)
+// Exact pruning needs spatially compact candidate blocks and query groups.  The rows are
+// ordered by a few Lloyd iterations of k-means (KM_K centroids) on a 32-dimensional +-1
+// random projection of the bf16 rows, then by the first projected coordinate: clustered data
+// (embeddings) lands in runs of one cluster each.  The order only decides how much is
+// pruned; every skip below is proven with FP64 balls, whatever the order.  (A random-
+// projection tree with median splits was tried first: in 128 dimensions a single projection
+// crowds 200 clusters together and every split cuts through dozens of them.)
+constexpr int KM_P = 32;   // projected dimensions
+constexpr int KM_K = 1024;  // centroids (several per cluster: a cluster without a seed merges)
+constexpr int KM_IT = 4;   // Lloyd iterations
+
+__device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ uint32_t f32_order(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// Y[i] = R x_i, R[p][j] = +-1 (hash of p and j)
+__global__ __launch_bounds__(256) void km_project_kernel(const __bf16 *__restrict__ Xh, int DP, int d, int64_t n,
+                                                         float *__restrict__ Y) {
+    HDB_GRID_STRIDE(i, n) {
+        const __bf16 *x = Xh + i * DP;
+        float y[KM_P];
+#pragma unroll
+        for (int p = 0; p < KM_P; p++) y[p] = 0.f;
+        for (int j0 = 0; j0 < d; j0 += 8) {
+            const bf16x8 v = *(const bf16x8 *)(x + j0);  // zero past d (DP padding)
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const float f = (float)v[u];
+                const uint32_t sg = hash_u32((uint32_t)(j0 + u) * 0x9E3779B1u + 0x5bd1e995u);
+#pragma unroll
+                for (int p = 0; p < KM_P; p++) y[p] += ((sg >> p) & 1u) ? -f : f;
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < KM_P; p++) Y[i * KM_P + p] = y[p];
+    }
+}
+
+// initial centroids: KM_K rows spread over the input
+__global__ void km_init_kernel(const float *__restrict__ Y, int64_t n, float *__restrict__ C) {  // grid: k
+    const int c = blockIdx.x, p = threadIdx.x;
+    const int64_t r = (int64_t)(((unsigned long long)hash_u32(c * 2654435761u + 17u) * (unsigned long long)n) >> 32);
+    C[c * KM_P + p] = Y[r * KM_P + p];
+}
+
+// nearest centroid of every row (centroids staged in LDS); sums by global atomics
+__global__ __launch_bounds__(512) void km_assign_kernel(const float *__restrict__ Y, int64_t n, int k,
+                                                        const float *__restrict__ C, int *__restrict__ asg,
+                                                        float *__restrict__ sum, float *__restrict__ cnt,
+                                                        int *__restrict__ hist) {
+    __shared__ float c_s[KM_K * KM_P];
+    for (int i = threadIdx.x; i < k * KM_P; i += blockDim.x) c_s[i] = C[i];
+    __syncthreads();
+    HDB_GRID_STRIDE(i, n) {
+        float y[KM_P];
+#pragma unroll
+        for (int p = 0; p < KM_P; p++) y[p] = Y[i * KM_P + p];
+        float best = INFINITY;
+        int bc = 0;
+        for (int c = 0; c < k; c++) {
+            float s2 = 0.f;
+#pragma unroll
+            for (int p = 0; p < KM_P; p++) {
+                const float e = y[p] - c_s[c * KM_P + p];
+                s2 = fmaf(e, e, s2);
+            }
+            if (s2 < best) {
+                best = s2;
+                bc = c;
+            }
+        }
+        asg[i] = bc;
+        if (hist) atomicAdd(&hist[bc], 1);
+        if (sum) {
+#pragma unroll
+            for (int p = 0; p < KM_P; p++) atomicAdd(&sum[bc * KM_P + p], y[p]);
+            atomicAdd(&cnt[bc], 1.f);
+        }
+    }
+}
+
+__global__ void km_update_kernel(float *__restrict__ C, float *__restrict__ sum, float *__restrict__ cnt) {
+    const int c = blockIdx.x, p = threadIdx.x;
+    const float k = cnt[c];
+    if (k > 0.f) C[c * KM_P + p] = sum[c * KM_P + p] / k;
+    __syncthreads();
+    sum[c * KM_P + p] = 0.f;
+    if (p == 0) cnt[c] = 0.f;
+}
+
+__global__ void km_keys_kernel(const float *__restrict__ Y, const int *__restrict__ asg, int64_t n,
+                               unsigned long long *__restrict__ keys, int *__restrict__ vals) {
+    HDB_GRID_STRIDE(i, n) {
+        keys[i] = ((unsigned long long)asg[i] << 32) | f32_order(Y[i * KM_P]);
+        vals[i] = (int)i;
+    }
+}
+
+// Ball of G consecutive rows of the order (FP64, scaled domain v = (x - mu) sc, exactly as
+// split_rows_kernel computes v): centre, radius and max norm, both rounded up.  One
+// workgroup per group.
+__global__ __launch_bounds__(256) void ball_kernel(const double *__restrict__ X, int d, const double *__restrict__ mu,
+                                                   const double *__restrict__ prm, const int *__restrict__ perm,
+                                                   const int *__restrict__ g_blk, const int *__restrict__ g_nblk,
+                                                   int64_t G, int DPc, double *__restrict__ ctr,
+                                                   double *__restrict__ rn) {
+    __shared__ double m_s[256];
+    __shared__ double r_s[256], q_s[256];
+    const int tid = threadIdx.x;
+    const double sc = prm[1];
+    // rows [r0, r1) of the layout (padding rows, perm < 0, are not part of the ball)
+    const int64_t r0 = g_blk ? (int64_t)g_blk[blockIdx.x] * 32 : (int64_t)blockIdx.x * G;
+    const int64_t r1 = g_blk ? r0 + (int64_t)g_nblk[blockIdx.x] * 32 : r0 + G;
+    int64_t cnt = 0;
+    for (int64_t r = r0; r < r1; r++) cnt += perm[r] >= 0;
+    if (cnt == 0) {
+        for (int c = tid; c < DPc; c += 256) ctr[(int64_t)blockIdx.x * DPc + c] = 0.0;
+        if (tid == 0) rn[2 * blockIdx.x] = rn[2 * blockIdx.x + 1] = 0.0;
+        return;
+    }
+    for (int c = tid; c < d; c += 256) {
+        double sum = 0.0;
+        for (int64_t r = r0; r < r1; r++)
+            if (perm[r] >= 0) sum += (X[(int64_t)perm[r] * d + c] - mu[c]) * sc;
+        m_s[c] = sum / (double)cnt;
+    }
+    __syncthreads();
+    for (int c = tid; c < DPc; c += 256) ctr[(int64_t)blockIdx.x * DPc + c] = c < d ? m_s[c] : 0.0;
+    double md = 0.0, mn = 0.0;
+    for (int64_t r = r0 + tid; r < r1; r += 256) {
+        if (perm[r] < 0) continue;
+        const double *x = X + (int64_t)perm[r] * d;
+        double a = 0.0, b = 0.0;
+        for (int c = 0; c < d; c++) {
+            const double v = (x[c] - mu[c]) * sc, e = v - m_s[c];
+            a += e * e;
+            b += v * v;
+        }
+        md = fmax(md, a);
+        mn = fmax(mn, b);
+    }
+    r_s[tid] = md;
+    q_s[tid] = mn;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) {
+            r_s[tid] = fmax(r_s[tid], r_s[tid + o]);
+            q_s[tid] = fmax(q_s[tid], q_s[tid + o]);
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        rn[2 * blockIdx.x] = sqrt(r_s[0]) * (1.0 + 1e-12) + 1e-300;
+        rn[2 * blockIdx.x + 1] = sqrt(q_s[0]) * (1.0 + 1e-12) + 1e-300;
+    }
+}
+
 typedef __attribute__((address_space(3))) void *lds_ptr_t;
+
+// candidate superblocks (runs of consecutive 32-row blocks of the layout) and their balls
+constexpr int NSB_MAX = 2048;
+struct SbArgs {
+    const double *qctr, *qrn;  // query-group balls (one per workgroup)
+    const double *sctr, *srn;  // superblock balls
+    const int *sb_blk;         // first block of each superblock
+    const int *sb_nblk;        // blocks of each superblock
+    const int *perm;           // layout position -> row of X (-1: padding row)
+    int nsb;                   // superblocks (<= NSB_MAX)
+    int prune;                 // 0: every superblock in index order
+    unsigned long long *blocks_done;
+};
 
 template <int DP, int KC>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void knn_mfma_screen_kernel(
     const __bf16 *__restrict__ Xh, const __bf16 *__restrict__ Xl, const double *__restrict__ nrm2,
     const double *__restrict__ nrm, const float *__restrict__ cst, int64_t n, int64_t n_pad, int excl,
-    LogEnt *__restrict__ logs, int *__restrict__ log_cnt, float *__restrict__ thr_out, int *__restrict__ overflow) {
+    LogEnt *__restrict__ logs, int *__restrict__ log_cnt, float *__restrict__ thr_out, int *__restrict__ overflow,
+    SbArgs sb) {
     using C = ScreenCfg<DP>;
     constexpr int QT = C::QT, SQ = C::SQ, CH = C::CH, BUF = C::BUF, NS = DP / KS;
     // two distinct LDS objects per double buffer: the compiler's waitcnt pass then knows the
@@ -425,8 +609,21 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __shared__ int cnt_s[SQ];
     __shared__ double qn2_s[SQ], qn_s[SQ];
 
+    __shared__ float sk_s[NSB_MAX];           // superblock keys (lower bound - 2 max bound), ascending
+    __shared__ unsigned short si_s[NSB_MAX];  // superblock ids in key order
+    __shared__ float tmax_s[2][NW];           // per-wave max thr, written in alternate iterations
+
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, half = lane >> 5, col = lane & 31;
     const int64_t qbase = (int64_t)blockIdx.x * SQ;
+    {
+        // a group of padding rows only (uniform: every thread reads the same rows)
+        bool any = false;
+        for (int i = 0; i < SQ && !any; i += 32) any = sb.perm[qbase + i] >= 0;
+        if (!any) {
+            for (int i = tid; i < SQ; i += 64 * NW) log_cnt[qbase + i] = 0;
+            return;
+        }
+    }
     const double eps_dot = 2.0 * (3.1 * 0x1p-16 + 3.0 * DP * 0x1p-24) * 1.01;
     const float epsf = (float)eps_dot * 1.001f;
     const bool ex = excl != 0;
@@ -437,13 +634,68 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         qn2_s[i] = nrm2[qbase + i];
         qn_s[i] = nrm[qbase + i];
     }
+    // superblock visiting order: ascending lower bound of (FP64 ball gap)^2 minus twice the
+    // largest screen bound; a superblock whose key exceeds every query's thr holds no
+    // candidate any query could log (lb >= exact - 2 bound >= gap^2 - 2 bound > thr)
+    int nsbp = 1;
+    while (nsbp < sb.nsb) nsbp <<= 1;
+    if (sb.prune) {
+        const double *mq = sb.qctr + (int64_t)blockIdx.x * DP;
+        const double RQ = sb.qrn[2 * blockIdx.x], NQ = sb.qrn[2 * blockIdx.x + 1];
+        for (int i = tid; i < nsbp; i += 64 * NW) {
+            float key = INFINITY;
+            if (i < sb.nsb) {
+                const double *ms = sb.sctr + (int64_t)i * DP;
+                double d2 = 0.0;
+                for (int c = 0; c < DP; c++) {
+                    const double e = mq[c] - ms[c];
+                    d2 += e * e;
+                }
+                const double RS = sb.srn[2 * i], NS = sb.srn[2 * i + 1];
+                const double gap = sqrt(d2) * (1.0 - 1e-12) - (RQ + RS) * (1.0 + 1e-12);
+                const double lb2 = gap > 0.0 ? gap * gap * (1.0 - 1e-12) : 0.0;
+                const double bm = eps_dot * NQ * NS + 4e-13 * (NQ * NQ + NS * NS) + 1e-30;
+                key = f32_down(lb2 - 2.0 * bm * (1.0 + 1e-12));
+            }
+            sk_s[i] = key;
+            si_s[i] = (unsigned short)i;
+        }
+        __syncthreads();
+        for (int k = 2; k <= nsbp; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = tid; i < nsbp; i += 64 * NW) {
+                    const int ij = i ^ j;
+                    if (ij > i) {
+                        const bool up = (i & k) == 0;
+                        const float x = sk_s[i], y = sk_s[ij];
+                        if ((x > y) == up) {
+                            sk_s[i] = y;
+                            sk_s[ij] = x;
+                            const unsigned short t = si_s[i];
+                            si_s[i] = si_s[ij];
+                            si_s[ij] = t;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+    } else {
+        for (int i = tid; i < nsbp; i += 64 * NW) {
+            sk_s[i] = -INFINITY;
+            si_s[i] = (unsigned short)i;
+        }
+    }
+    if (tid < 2 * NW) tmax_s[tid / NW][tid % NW] = INFINITY;
+
     bf16x8 bh[QT][NS], bl[QT][NS];
     float g[QT], qh[QT], a[QT];
     int qloc[QT];
+    bool qv[QT];  // a real row (not padding)
 #pragma unroll
     for (int t = 0; t < QT; t++) {
         qloc[t] = wave * 32 * QT + 32 * t + col;
         const int64_t row = qbase + qloc[t];
+        qv[t] = sb.perm[row] >= 0;
 #pragma unroll
         for (int s = 0; s < NS; s++) {
             const int64_t o = row * DP + KS * s + 8 * half;
@@ -483,15 +735,31 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                                              (lds_ptr_t)cstb(B), 16, 0, 0);
     };
 
-    const int64_t nblk = n_pad / 32;  // even (n_pad is a multiple of 512)
-    using B0 = std::integral_constant<int, 0>;
-    using B1 = std::integral_constant<int, 1>;
-    auto step = [&](auto B, auto Bn, int64_t blk) {
-        const int64_t cb = blk * 32;
+    // the block sequence: superblocks in key order while key <= max thr of the group (read
+    // one iteration late from alternating slots, so every wave takes the same decision)
+    auto sb_blocks = [&](int i) -> int {
+        return sb.sb_nblk[si_s[i]];
+    };
+    float wmax = INFINITY;  // this wave's max thr over its real queries (uniform)
+    int par = 0;
+    int ci_sb = 0, ci_b = 0;  // current superblock (key order) and block within it; -1: done
+    int64_t nproc = 0;
+    auto step = [&](auto B, auto Bn) {
+        const int64_t cb = ((int64_t)sb.sb_blk[si_s[ci_sb]] + ci_b) * 32;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // block blk landed everywhere; block blk-1's buffer is free
-        if (blk + 1 < nblk) stage(Bn, cb + 32);
+        __syncthreads();  // block landed everywhere; the other buffer is free
+        float thrmax = tmax_s[par ^ 1][0];
+#pragma unroll
+        for (int w = 1; w < NW; w++) thrmax = fmaxf(thrmax, tmax_s[par ^ 1][w]);
+        int nx_sb = ci_sb, nx_b = ci_b + 1;
+        if (nx_b >= sb_blocks(ci_sb)) {
+            nx_sb = ci_sb + 1;
+            nx_b = 0;
+            if (!(nx_sb < sb.nsb && sk_s[nx_sb] <= thrmax)) nx_sb = -1;
+        }
+        if (nx_sb >= 0) stage(Bn, ((int64_t)sb.sb_blk[si_s[nx_sb]] + nx_b) * 32);
         float *const cst_s = cstb(B);
+        nproc++;
 
         const __bf16 *hb = cbuf(B), *lb = hb + 32 * DP;
         f32x16 acc[QT];
@@ -539,7 +807,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     for (int t = 0; t < QT; t++) {
                         const int ql = qloc[t];
                         const int64_t qid = qbase + ql;
-                        if (!(m[t] >= a[t]) || qid >= n) continue;
+                        if (!(m[t] >= a[t]) || !qv[t]) continue;
                         const double q2 = qn2_s[ql], qn = qn_s[ql];
                         float *tp = top_s + ql * KC;
 #pragma unroll 1
@@ -548,7 +816,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                             const float av = acc[t][r];  // dynamic element (rare path)
                             const float v = fmaf(g[t], cst_s[32 + ci], av) - cst_s[ci];
                             const int64_t cid = cb + ci;
-                            if (!(v >= a[t]) || cid >= n || (ex && cid == qid)) continue;
+                            if (!(v >= a[t]) || (ex && cid == qid) || sb.perm[cid] < 0) continue;
                             const double c2 = c2d[ci], cn = cnd[ci];
                             const double approx = (q2 + c2) - 2.0 * (double)av;
                             const double bound = eps_dot * qn * cn + 4e-13 * (q2 + c2) + 1e-30;
@@ -582,19 +850,38 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 }
                 __builtin_amdgcn_wave_barrier();
             }
+            float wm = -INFINITY;
 #pragma unroll
-            for (int t = 0; t < QT; t++) a[t] = qh[t] - 0.5f * top_s[qloc[t] * KC + KC - 1];
+            for (int t = 0; t < QT; t++) {
+                const float th = top_s[qloc[t] * KC + KC - 1];
+                a[t] = qh[t] - 0.5f * th;
+                if (qv[t]) wm = fmaxf(wm, th);
+            }
+            for (int o = 32; o >= 1; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o));
+            wmax = wm;
         }
+        if (lane == 0) tmax_s[par][wave] = wmax;
+        par ^= 1;
+        ci_sb = nx_sb;
+        ci_b = nx_b;
     };
-    stage(B0{}, 0);
-    for (int64_t blk = 0; blk < nblk; blk += 2) {
-        step(B0{}, B1{}, blk);
-        step(B1{}, B0{}, blk + 1);
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    __syncthreads();
+    stage(B0{}, (int64_t)sb.sb_blk[si_s[0]] * 32);
+    while (true) {
+        step(B0{}, B1{});
+        if (ci_sb < 0) break;
+        step(B1{}, B0{});
+        if (ci_sb < 0) break;
     }
+    if (sb.blocks_done && tid == 0) atomicAdd(sb.blocks_done, (unsigned long long)nproc);
     __syncthreads();
     for (int i = tid; i < SQ; i += 64 * NW) {
         const int64_t qid = qbase + i;
-        if (qid < n) {
+        if (sb.perm[qid] < 0) {
+            log_cnt[qid] = 0;
+        } else {
             log_cnt[qid] = cnt_s[i] > S_LOGCAP ? -1 : cnt_s[i];
             thr_out[qid] = top_s[i * KC + KC - 1];
         }
@@ -608,18 +895,20 @@ __global__ __launch_bounds__(256) void knn_mfma_final_kernel(const double *__res
                                                              const LogEnt *__restrict__ logs,
                                                              const int *__restrict__ log_cnt,
                                                              const float *__restrict__ thr,
+                                                             const int *__restrict__ perm,
                                                              double *__restrict__ lists) {
     const int lane = threadIdx.x & 63;
     const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (q >= n) return;
+    if (q >= n || perm[q] < 0) return;  // n: layout rows here
     const int cnt = log_cnt[q];
     const float t = thr[q];
+    const int64_t qo = perm[q];  // the query's row in X (the lists follow X's order)
     double top[KC];
 #pragma unroll
     for (int k = 0; k < KC; k++) top[k] = INFINITY;
     for (int j = lane; j < cnt; j += 64) {
         const LogEnt e = logs[q * S_LOGCAP + j];
-        if (e.lb <= t) topk_insert<KC>(top, exact_sq<0>(X + q * d, X + (int64_t)e.cid * d, d));
+        if (e.lb <= t) topk_insert<KC>(top, exact_sq<0>(X + qo * d, X + (int64_t)perm[e.cid] * d, d));
     }
     for (int k = 0; k < KC; k++) {
         double mn = top[0];
@@ -630,7 +919,7 @@ __global__ __launch_bounds__(256) void knn_mfma_final_kernel(const double *__res
             for (int i = 0; i + 1 < KC; i++) top[i] = top[i + 1];
             top[KC - 1] = INFINITY;
         }
-        if (lane == 0) lists[q * KC + k] = (mn < INFINITY) ? sqrt(mn) : JMAX;
+        if (lane == 0) lists[qo * KC + k] = (mn < INFINITY) ? sqrt(mn) : JMAX;
     }
 }
 
@@ -638,31 +927,117 @@ __global__ __launch_bounds__(256) void knn_mfma_final_kernel(const double *__res
 template <int DP, int KC>
 static void launch_single(hdb_ctx *ctx, const double *X, int64_t n, int64_t n_pad, int d, const __bf16 *Xh,
                           const __bf16 *Xl, const double *nrm2, const double *nrm, const float *cst, int excl,
-                          LogEnt *logs, int *log_cnt, float *thr, int *overflow, double *lists) {
+                          LogEnt *logs, int *log_cnt, float *thr, int *overflow, const int *perm, const SbArgs &sb,
+                          double *lists) {
     hipStream_t st = ctx->stream;
     using C = ScreenCfg<DP>;
     {
         KernelTimer t(ctx, "knn_mfma");
         hipLaunchKernelGGL((knn_mfma_screen_kernel<DP, KC>), dim3((unsigned)(n_pad / C::SQ)), dim3(64 * NW), 0, st, Xh,
-                           Xl, nrm2, nrm, cst, n, n_pad, excl, logs, log_cnt, thr, overflow);
+                           Xl, nrm2, nrm, cst, n, n_pad, excl, logs, log_cnt, thr, overflow, sb);
         HIP_CHECK(hipGetLastError());
     }
     {
         KernelTimer t(ctx, "knn_mfma_final");
         hipLaunchKernelGGL((knn_mfma_final_kernel<KC>), dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, X, n, d,
-                           logs, log_cnt, thr, lists);
+                           logs, log_cnt, thr, perm, lists);
         HIP_CHECK(hipGetLastError());
     }
+}
+
+__global__ void order_iota_kernel(int *p, int64_t n, int64_t n_pad) {
+    HDB_GRID_STRIDE(i, n_pad) p[i] = i < n ? (int)i : -1;
+}
+
+// sorted position p (cluster c = key >> 32, rank p - start[c]) -> layout position off[c] + rank
+__global__ void km_scatter_kernel(const unsigned long long *__restrict__ keys, const int *__restrict__ rows, int64_t n,
+                                  const int *__restrict__ start, const int *__restrict__ off, int *__restrict__ perm) {
+    HDB_GRID_STRIDE(p, n) {
+        const int c = (int)(keys[p] >> 32);
+        perm[(int64_t)off[c] + (p - start[c])] = rows[p];
+    }
+}
+
+// number of k-means centroids for n rows (every cluster is padded to a multiple of 256 rows)
+static int km_k(int64_t n) { return (int)std::min<int64_t>(KM_K, std::max<int64_t>(1, n / 2048)); }
+
+struct KmBufs {
+    unsigned long long *k1, *k2;
+    int *vals, *rows, *asg, *hist, *start, *off;
+    float *Y, *C, *sum, *cnt;
+    void *tmp;
+    size_t tmp_bytes;
+};
+
+// The candidate layout: rows of each k-means cluster in consecutive positions (ordered by the
+// first projected coordinate), every cluster padded to a multiple of 256 rows (perm = -1), so
+// no query group and no block mixes clusters.  Superblocks: each cluster's blocks in runs of
+// at most sbmax.  Returns the layout's row count (a multiple of 256).
+static int64_t km_layout(hdb_ctx *ctx, const __bf16 *Xh, int DP, int d, int64_t n, const KmBufs &b, int *perm,
+                         std::vector<int> &sb_blk, std::vector<int> &sb_nblk) {
+    hipStream_t st = ctx->stream;
+    KernelTimer t(ctx, "knn_mfma_order");
+    const int k = km_k(n);
+    const int g = (int)std::min<int64_t>(ceil_div(n, 256), 8192);
+    hipLaunchKernelGGL(km_project_kernel, dim3(g), dim3(256), 0, st, Xh, DP, d, n, b.Y);
+    hipLaunchKernelGGL(km_init_kernel, dim3(k), dim3(KM_P), 0, st, b.Y, n, b.C);
+    HIP_CHECK(hipMemsetAsync(b.sum, 0, 4 * (size_t)KM_K * KM_P, st));
+    HIP_CHECK(hipMemsetAsync(b.cnt, 0, 4 * (size_t)KM_K, st));
+    HIP_CHECK(hipMemsetAsync(b.hist, 0, 4 * (size_t)KM_K, st));
+    const int ga = (int)std::min<int64_t>(ceil_div(n, 512), 1024);
+    for (int it = 0; it < KM_IT; it++) {
+        hipLaunchKernelGGL(km_assign_kernel, dim3(ga), dim3(512), 0, st, b.Y, n, k, b.C, b.asg, b.sum, b.cnt,
+                           (int *)nullptr);
+        hipLaunchKernelGGL(km_update_kernel, dim3(k), dim3(KM_P), 0, st, b.C, b.sum, b.cnt);
+    }
+    hipLaunchKernelGGL(km_assign_kernel, dim3(ga), dim3(512), 0, st, b.Y, n, k, b.C, b.asg, (float *)nullptr,
+                       (float *)nullptr, b.hist);
+    HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(km_keys_kernel, dim3(g), dim3(256), 0, st, b.Y, b.asg, n, b.k1, b.vals);
+    size_t tb = b.tmp_bytes;
+    HIP_CHECK(sort_pairs(b.tmp, tb, b.k1, b.k2, b.vals, b.rows, n, 0, 48, st));  // KM_K <= 2^16
+    std::vector<int> hist(k), start(k), off(k);
+    HIP_CHECK(hipMemcpyAsync(hist.data(), b.hist, 4 * (size_t)k, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    int64_t s0 = 0, o0 = 0, nbr = 0, nz = 0;
+    for (int c = 0; c < k; c++) {
+        start[c] = (int)s0;
+        off[c] = (int)o0;
+        s0 += hist[c];
+        o0 += ceil_div((int64_t)hist[c], (int64_t)256) * 256;
+        nbr += ceil_div((int64_t)hist[c], (int64_t)32);
+        nz += hist[c] > 0;
+    }
+    const int64_t n_lay = o0;
+    const int sbmax = (int)std::max<int64_t>(1, ceil_div(nbr, std::max<int64_t>(1, NSB_MAX - nz)));
+    sb_blk.clear();
+    sb_nblk.clear();
+    for (int c = 0; c < k; c++) {
+        const int nb = (int)ceil_div((int64_t)hist[c], (int64_t)32);
+        for (int j = 0; j < nb; j += sbmax) {
+            sb_blk.push_back(off[c] / 32 + j);
+            sb_nblk.push_back(std::min(sbmax, nb - j));
+        }
+    }
+    HIP_CHECK(hipMemcpyAsync(b.start, start.data(), 4 * (size_t)k, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(b.off, off.data(), 4 * (size_t)k, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemsetAsync(perm, 0xff, 4 * (size_t)ceil_div(n_lay, (int64_t)512) * 512, st));
+    hipLaunchKernelGGL(km_scatter_kernel, dim3(g), dim3(256), 0, st, b.k2, b.rows, n, b.start, b.off, perm);
+    HIP_CHECK(hipStreamSynchronize(st));  // start/off staged from host vectors
+    return n_lay;
 }
 
 template <int DP>
 static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC, bool excl, double *lists) {
     const int64_t n_pad = ceil_div(n, (int64_t)512) * 512;  // multiple of MQ and of every SQ
+    const bool single = ctx->knn_mfma_single, prune = single && ctx->knn_mfma_prune;
+    // row capacity: the pruned layout pads every k-means cluster to a multiple of 256 rows
+    const int64_t n_cap = prune ? ceil_div(n + 256 * (int64_t)km_k(n), (int64_t)512) * 512 : n_pad;
     const int nb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, n / 64));
     auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t bytes = 2 * rnd(sizeof(__bf16) * (size_t)(n_pad * DP)) + 3 * rnd(8 * (size_t)n_pad) +
+    const size_t bytes = 2 * rnd(sizeof(__bf16) * (size_t)(n_cap * DP)) + 3 * rnd(8 * (size_t)n_cap) +
                          2 * rnd(8 * (size_t)nb * d) + rnd(8 * (size_t)d) + 256 + 256 +
-                         rnd(4 * (size_t)(n_pad / 32) * S_CST) + 2 * rnd(4 * (size_t)n_pad);
+                         rnd(4 * (size_t)(n_cap / 32) * S_CST) + 2 * rnd(4 * (size_t)n_cap);
     char *base = (char *)arena(ctx, A_WORK3, bytes);
     size_t off = 0;
     auto take = [&](size_t b) {
@@ -670,17 +1045,17 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
         off += rnd(b);
         return p;
     };
-    __bf16 *Xh = (__bf16 *)take(sizeof(__bf16) * (size_t)(n_pad * DP));
-    __bf16 *Xl = (__bf16 *)take(sizeof(__bf16) * (size_t)(n_pad * DP));
-    double *nrm2 = (double *)take(8 * (size_t)n_pad), *nrm = (double *)take(8 * (size_t)n_pad);
+    __bf16 *Xh = (__bf16 *)take(sizeof(__bf16) * (size_t)(n_cap * DP));
+    __bf16 *Xl = (__bf16 *)take(sizeof(__bf16) * (size_t)(n_cap * DP));
+    double *nrm2 = (double *)take(8 * (size_t)n_cap), *nrm = (double *)take(8 * (size_t)n_cap);
     double *psum = (double *)take(8 * (size_t)nb * d), *pmax = (double *)take(8 * (size_t)nb * d);
     double *mu = (double *)take(8 * (size_t)d);
-    double *thr = (double *)take(8 * (size_t)n_pad);
+    double *thr = (double *)take(8 * (size_t)n_cap);
     double *prm = (double *)take(256);
     unsigned long long *stats = (unsigned long long *)take(256);
-    float *cst = (float *)take(4 * (size_t)(n_pad / 32) * S_CST);
-    int *log_cnt = (int *)take(4 * (size_t)n_pad);
-    float *thr_f = (float *)take(4 * (size_t)n_pad);
+    float *cst = (float *)take(4 * (size_t)(n_cap / 32) * S_CST);
+    int *log_cnt = (int *)take(4 * (size_t)n_cap);
+    float *thr_f = (float *)take(4 * (size_t)n_cap);
     hipStream_t st = ctx->stream;
     hipLaunchKernelGGL(col_stats_kernel, dim3(nb), dim3(256), 0, st, X, n, d, nb, psum, pmax);
     hipLaunchKernelGGL(centre_kernel, dim3(1), dim3(256), 0, st, psum, pmax, nb, n, d, mu, prm);
@@ -691,19 +1066,108 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
     {
         const int g = (int)std::min<int64_t>(ceil_div(n_pad * 64, 256), 8192);
         hipLaunchKernelGGL(split_rows_kernel, dim3(g), dim3(256), 0, st, X, n, n_pad, d, DP, mu, prm, Xh, Xl, nrm2,
-                           nrm);
+                           nrm, nullptr);
     }
-    if (ctx->knn_mfma_single) {
-        const int g = (int)std::min<int64_t>(ceil_div(n_pad, 256), 4096);
-        hipLaunchKernelGGL(screen_consts_kernel, dim3(g), dim3(256), 0, st, nrm2, nrm, n_pad, cst);
-        LogEnt *logs = (LogEnt *)arena(ctx, A_LOG, sizeof(LogEnt) * (size_t)n_pad * S_LOGCAP);
+    if (single) {
+        using Cf = ScreenCfg<DP>;
+        // layout (A_ORDER): perm, k-means scratch, query-group and superblock balls
+        const int64_t n_sortcap = std::max<int64_t>(n, 1);
+        size_t sort_tb = 0;
+        HIP_CHECK(sort_pairs(nullptr, sort_tb, (const unsigned long long *)nullptr, (unsigned long long *)nullptr,
+                             (const int *)nullptr, (int *)nullptr, n_sortcap, 0, 64, st));
+        const size_t obytes = rnd(4 * (size_t)n_cap) + 3 * rnd(4 * (size_t)n) + 2 * rnd(8 * (size_t)n) +
+                              rnd(sort_tb) + rnd(4 * (size_t)n * KM_P) + 2 * rnd(4 * KM_K * KM_P) +
+                              rnd(4 * KM_K) + 3 * rnd(4 * KM_K) + rnd(8 * (size_t)(n_cap / 128) * DP) +
+                              rnd(16 * (size_t)(n_cap / 128)) + rnd(8 * (size_t)NSB_MAX * DP) + rnd(16 * NSB_MAX) +
+                              2 * rnd(4 * NSB_MAX);
+        char *ob = (char *)arena(ctx, A_ORDER, obytes);
+        size_t oo = 0;
+        auto otake = [&](size_t b) {
+            char *p = ob + oo;
+            oo += rnd(b);
+            return p;
+        };
+        int *perm = (int *)otake(4 * (size_t)n_cap);
+        KmBufs kb;
+        kb.vals = (int *)otake(4 * (size_t)n);
+        kb.rows = (int *)otake(4 * (size_t)n);
+        kb.asg = (int *)otake(4 * (size_t)n);
+        kb.k1 = (unsigned long long *)otake(8 * (size_t)n);
+        kb.k2 = (unsigned long long *)otake(8 * (size_t)n);
+        kb.tmp = otake(sort_tb);
+        kb.tmp_bytes = sort_tb;
+        kb.Y = (float *)otake(4 * (size_t)n * KM_P);
+        kb.C = (float *)otake(4 * KM_K * KM_P);
+        kb.sum = (float *)otake(4 * KM_K * KM_P);
+        kb.cnt = (float *)otake(4 * KM_K);
+        kb.hist = (int *)otake(4 * KM_K);
+        kb.start = (int *)otake(4 * KM_K);
+        kb.off = (int *)otake(4 * KM_K);
+        double *qctr = (double *)otake(8 * (size_t)(n_cap / 128) * DP);
+        double *qrn = (double *)otake(16 * (size_t)(n_cap / 128));
+        double *sctr = (double *)otake(8 * (size_t)NSB_MAX * DP), *srn = (double *)otake(16 * NSB_MAX);
+        int *sb_blk_d = (int *)otake(4 * NSB_MAX), *sb_nblk_d = (int *)otake(4 * NSB_MAX);
+        std::vector<int> sb_blk, sb_nblk;
+        int64_t n_lay = n;
+        if (prune) {
+            n_lay = km_layout(ctx, Xh, DP, d, n, kb, perm, sb_blk, sb_nblk);
+        } else {
+            const int g = (int)std::min<int64_t>(ceil_div(n_pad, 256), 8192);
+            hipLaunchKernelGGL(order_iota_kernel, dim3(g), dim3(256), 0, st, perm, n, n_pad);
+            const int64_t nbr = ceil_div(n, (int64_t)32);
+            const int sbb = (int)ceil_div(nbr, (int64_t)NSB_MAX);
+            for (int64_t b0 = 0; b0 < nbr; b0 += sbb) {
+                sb_blk.push_back((int)b0);
+                sb_nblk.push_back((int)std::min<int64_t>(sbb, nbr - b0));
+            }
+        }
+        const int64_t n_lp = ceil_div(n_lay, (int64_t)512) * 512;  // layout rows incl. padding
+        const int nsb = (int)sb_blk.size();
+        HIP_CHECK(hipMemcpyAsync(sb_blk_d, sb_blk.data(), 4 * (size_t)nsb, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(sb_nblk_d, sb_nblk.data(), 4 * (size_t)nsb, hipMemcpyHostToDevice, st));
+        if (prune) {
+            const int g = (int)std::min<int64_t>(ceil_div(n_lp * 64, 256), 8192);
+            hipLaunchKernelGGL(split_rows_kernel, dim3(g), dim3(256), 0, st, X, n, n_lp, d, DP, mu, prm, Xh, Xl, nrm2,
+                               nrm, perm);
+            hipLaunchKernelGGL(ball_kernel, dim3((unsigned)(n_lp / Cf::SQ)), dim3(256), 0, st, X, d, mu, prm, perm,
+                               (const int *)nullptr, (const int *)nullptr, (int64_t)Cf::SQ, DP, qctr, qrn);
+            hipLaunchKernelGGL(ball_kernel, dim3((unsigned)nsb), dim3(256), 0, st, X, d, mu, prm, perm, sb_blk_d,
+                               sb_nblk_d, (int64_t)0, DP, sctr, srn);
+        }
+        if (prune && ctx->count_evals) {
+            // diagnostic: ball radii (x 1e6, scaled domain) of query groups and superblocks
+            const int64_t nqg = n_lp / Cf::SQ;
+            std::vector<double> hq(2 * (size_t)nqg), hs(2 * (size_t)nsb);
+            HIP_CHECK(hipMemcpyAsync(hq.data(), qrn, 16 * (size_t)nqg, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipMemcpyAsync(hs.data(), srn, 16 * (size_t)nsb, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            auto med = [](const std::vector<double> &v) {
+                std::vector<double> r;
+                for (size_t i = 0; i < v.size(); i += 2)
+                    if (v[i] > 0) r.push_back(v[i]);
+                std::sort(r.begin(), r.end());
+                return r.empty() ? 0.0 : r[r.size() / 2];
+            };
+            ctx->stats["knn_mfma_qrad_med_e6"] = (int64_t)(med(hq) * 1e6);
+            ctx->stats["knn_mfma_sbrad_med_e6"] = (int64_t)(med(hs) * 1e6);
+            ctx->stats["knn_mfma_nsb"] = nsb;
+            ctx->stats["knn_mfma_layout_rows"] = n_lay;
+        }
+        unsigned long long *blocks_done = stats + 1;
+        HIP_CHECK(hipMemsetAsync(blocks_done, 0, 8, st));
+        const SbArgs sbargs{qctr, qrn, sctr, srn, sb_blk_d, sb_nblk_d, perm, nsb, prune ? 1 : 0, blocks_done};
+        {
+            const int g = (int)std::min<int64_t>(ceil_div(n_lp, 256), 4096);
+            hipLaunchKernelGGL(screen_consts_kernel, dim3(g), dim3(256), 0, st, nrm2, nrm, n_lp, perm, cst);
+        }
+        LogEnt *logs = (LogEnt *)arena(ctx, A_LOG, sizeof(LogEnt) * (size_t)n_lp * S_LOGCAP);
         int *overflow = (int *)stats;
         HIP_CHECK(hipMemsetAsync(overflow, 0, 4, st));
         const int fl = excl ? 1 : 0;
 #define K1S_CASE(KK)                                                                                              \
     case KK:                                                                                                      \
-        launch_single<DP, KK>(ctx, X, n, n_pad, d, Xh, Xl, nrm2, nrm, cst, fl, logs, log_cnt, thr_f, overflow, \
-                              lists);                                                                             \
+        launch_single<DP, KK>(ctx, X, n_lp, n_lp, d, Xh, Xl, nrm2, nrm, cst, fl, logs, log_cnt, thr_f, overflow, \
+                              perm, sbargs, lists);                                                               \
         break;
         switch (KC) {
             K1S_CASE(1)
@@ -714,13 +1178,16 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
         default: return false;
         }
 #undef K1S_CASE
-        int h_ovf = 0;
-        HIP_CHECK(hipMemcpyAsync(&h_ovf, overflow, 4, hipMemcpyDeviceToHost, st));
+        unsigned long long h_st[2] = {0, 0};
+        HIP_CHECK(hipMemcpyAsync(h_st, stats, 16, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
+        const int h_ovf = (int)(h_st[0] & 0xffffffffull);
+        ctx->stats["knn_mfma_blocks"] = (int64_t)h_st[1];  // (query group, 32-candidate block) pairs computed
+        ctx->stats["knn_mfma_group_rows"] = Cf::SQ;
         if (ctx->count_evals) {
             // diagnostic: logged candidates (the FP64 re-checks are those with lb <= thr)
-            std::vector<int> hc((size_t)n);
-            HIP_CHECK(hipMemcpy(hc.data(), log_cnt, 4 * (size_t)n, hipMemcpyDeviceToHost));
+            std::vector<int> hc((size_t)n_lp);
+            HIP_CHECK(hipMemcpy(hc.data(), log_cnt, 4 * (size_t)n_lp, hipMemcpyDeviceToHost));
             int64_t tot = 0;
             for (int v : hc) tot += v < 0 ? S_LOGCAP : v;
             ctx->stats["knn_mfma_rechecks"] = tot;
@@ -728,7 +1195,11 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
         }
         ctx->stats["knn_mfma_log_overflow"] = h_ovf;
         if (h_ovf == 0) return true;
-        // a query's log overflowed (e.g. hundreds of exact duplicates): two-pass kernel for all
+        // a query's log overflowed (e.g. hundreds of exact duplicates): two-pass kernel for all,
+        // on the rows in their own order
+        const int g2 = (int)std::min<int64_t>(ceil_div(n_pad * 64, 256), 8192);
+        hipLaunchKernelGGL(split_rows_kernel, dim3(g2), dim3(256), 0, st, X, n, n_pad, d, DP, mu, prm, Xh, Xl, nrm2,
+                           nrm, nullptr);
     }
     if (ctx->count_evals) HIP_CHECK(hipMemsetAsync(stats, 0, 8, st));
     {

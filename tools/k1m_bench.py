@@ -33,17 +33,36 @@ torch.cuda.synchronize()
 ctx.set_timing(True)
 ctx.kernel_time("knn_mfma")
 ctx.kernel_time("knn_mfma_final")
+ctx.kernel_time("knn_mfma_order")
 t0 = time.perf_counter()
 L = star.knn(X, k, None, exclSelf=True)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 ms, _ = ctx.kernel_time("knn_mfma")
 ms_final, _ = ctx.kernel_time("knn_mfma_final")
+ms_order, _ = ctx.kernel_time("knn_mfma_order")
 ovf = ctx.get_stat("knn_mfma_log_overflow") if SINGLE else 0
 ctx.set_timing(False)
 if os.environ.get("K1M_QUICK"):
-    print(json.dumps({"n": n, "d": d, "lib": os.environ.get("HDBMI_LIB", "default"), "wall_s": dt, "knn_mfma_ms": ms,
-                      "knn_mfma_final_ms": ms_final}))
+    nb = ctx.get_stat("knn_mfma_blocks")
+    rows = ctx.get_stat("knn_mfma_group_rows")
+    n_pad = -(-n // 512) * 512
+    out = {"n": n, "d": d, "lib": os.environ.get("HDBMI_LIB", "default"), "wall_s": dt, "knn_mfma_ms": ms,
+           "knn_mfma_final_ms": ms_final, "knn_mfma_order_ms": ms_order, "blocks": nb,
+           "block_frac": nb * rows * 32 / (n * n_pad)}
+    if os.environ.get("K1M_DIAG"):
+        ctx.set_option("count_evals", 1)
+        star.knn(X, k, None, exclSelf=True)
+        ctx.set_option("count_evals", 0)
+        for key in ("knn_mfma_qrad_med_e6", "knn_mfma_sbrad_med_e6", "knn_mfma_nsb", "knn_mfma_rechecks",
+                    "knn_mfma_layout_rows"):
+            out[key] = ctx.get_stat(key)
+        import math
+        mu = X.mean(0)
+        sc = 2.0 ** -math.frexp(float((X - mu).abs().max()))[1]
+        out["scale"] = sc
+        out["kth_dist_scaled_med"] = float(L[:, -1].median()) * sc
+    print(json.dumps(out))
     sys.exit(0)
 ctx.set_option("count_evals", 1)
 star.knn(X[: min(n, 200_000)].contiguous(), k, None, exclSelf=True)
