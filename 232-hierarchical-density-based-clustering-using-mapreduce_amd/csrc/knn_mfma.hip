@@ -457,14 +457,15 @@ __global__ void km_init_kernel(const float *__restrict__ Y, int64_t n, float *__
 }
 
 // nearest centroid of every row (centroids staged in LDS); sums by global atomics
-__global__ __launch_bounds__(512) void km_assign_kernel(const float *__restrict__ Y, int64_t n, int k,
+__global__ __launch_bounds__(512) void km_assign_kernel(const float *__restrict__ Y, int64_t n, int64_t step, int k,
                                                         const float *__restrict__ C, int *__restrict__ asg,
                                                         float *__restrict__ sum, float *__restrict__ cnt,
                                                         int *__restrict__ hist) {
     __shared__ float c_s[KM_K * KM_P];
     for (int i = threadIdx.x; i < k * KM_P; i += blockDim.x) c_s[i] = C[i];
     __syncthreads();
-    HDB_GRID_STRIDE(i, n) {
+    HDB_GRID_STRIDE(ii, n) {
+        const int64_t i = ii * step;  // the Lloyd iterations run on a strided sample
         float y[KM_P];
 #pragma unroll
         for (int p = 0; p < KM_P; p++) y[p] = Y[i * KM_P + p];
@@ -799,24 +800,38 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
         for (int t = 0; t < QT; t++) hit |= m[t] >= a[t];
         if (__ballot(hit)) {
-            // rare: the two half-waves hold the same queries, so they take turns
+            // rare: the two half-waves hold the same queries, so they take turns; each lane
+            // walks only the set bits of its pass mask
             const double *c2d = (const double *)(cst_s + 64), *cnd = (const double *)(cst_s + 128);
+            unsigned hm[QT];
+#pragma unroll
+            for (int t = 0; t < QT; t++) {
+                hm[t] = 0u;
+                if (m[t] >= a[t] && qv[t]) {
+#pragma unroll
+                    for (int gi = 0; gi < 4; gi++) {
+                        const float4 h4 = hc4[2 * gi + half], c4 = cn4[2 * gi + half];
+                        hm[t] |= (fmaf(g[t], c4.x, acc[t][4 * gi + 0]) - h4.x >= a[t]) ? 1u << (4 * gi + 0) : 0u;
+                        hm[t] |= (fmaf(g[t], c4.y, acc[t][4 * gi + 1]) - h4.y >= a[t]) ? 1u << (4 * gi + 1) : 0u;
+                        hm[t] |= (fmaf(g[t], c4.z, acc[t][4 * gi + 2]) - h4.z >= a[t]) ? 1u << (4 * gi + 2) : 0u;
+                        hm[t] |= (fmaf(g[t], c4.w, acc[t][4 * gi + 3]) - h4.w >= a[t]) ? 1u << (4 * gi + 3) : 0u;
+                    }
+                }
+            }
             for (int h = 0; h < 2; h++) {
                 if (half == h) {
 #pragma unroll
                     for (int t = 0; t < QT; t++) {
                         const int ql = qloc[t];
                         const int64_t qid = qbase + ql;
-                        if (!(m[t] >= a[t]) || !qv[t]) continue;
                         const double q2 = qn2_s[ql], qn = qn_s[ql];
                         float *tp = top_s + ql * KC;
-#pragma unroll 1
-                        for (int r = 0; r < 16; r++) {
+                        for (unsigned mk = hm[t]; mk; mk &= mk - 1) {
+                            const int r = __builtin_ctz(mk);
                             const int ci = 8 * (r >> 2) + 4 * half + (r & 3);
                             const float av = acc[t][r];  // dynamic element (rare path)
-                            const float v = fmaf(g[t], cst_s[32 + ci], av) - cst_s[ci];
                             const int64_t cid = cb + ci;
-                            if (!(v >= a[t]) || (ex && cid == qid) || sb.perm[cid] < 0) continue;
+                            if ((ex && cid == qid) || sb.perm[cid] < 0) continue;
                             const double c2 = c2d[ci], cn = cnd[ci];
                             const double approx = (q2 + c2) - 2.0 * (double)av;
                             const double bound = eps_dot * qn * cn + 4e-13 * (q2 + c2) + 1e-30;
@@ -984,14 +999,17 @@ static int64_t km_layout(hdb_ctx *ctx, const __bf16 *Xh, int DP, int d, int64_t 
     HIP_CHECK(hipMemsetAsync(b.sum, 0, 4 * (size_t)KM_K * KM_P, st));
     HIP_CHECK(hipMemsetAsync(b.cnt, 0, 4 * (size_t)KM_K, st));
     HIP_CHECK(hipMemsetAsync(b.hist, 0, 4 * (size_t)KM_K, st));
-    const int ga = (int)std::min<int64_t>(ceil_div(n, 512), 1024);
+    // Lloyd iterations on a strided sample of <= 128k rows, then every row once
+    const int64_t step = std::max<int64_t>(1, n / 131072), m = n / step;
+    const int gs = (int)std::min<int64_t>(ceil_div(m, 512), 1024);
     for (int it = 0; it < KM_IT; it++) {
-        hipLaunchKernelGGL(km_assign_kernel, dim3(ga), dim3(512), 0, st, b.Y, n, k, b.C, b.asg, b.sum, b.cnt,
+        hipLaunchKernelGGL(km_assign_kernel, dim3(gs), dim3(512), 0, st, b.Y, m, step, k, b.C, b.asg, b.sum, b.cnt,
                            (int *)nullptr);
         hipLaunchKernelGGL(km_update_kernel, dim3(k), dim3(KM_P), 0, st, b.C, b.sum, b.cnt);
     }
-    hipLaunchKernelGGL(km_assign_kernel, dim3(ga), dim3(512), 0, st, b.Y, n, k, b.C, b.asg, (float *)nullptr,
-                       (float *)nullptr, b.hist);
+    const int ga = (int)std::min<int64_t>(ceil_div(n, 512), 1024);
+    hipLaunchKernelGGL(km_assign_kernel, dim3(ga), dim3(512), 0, st, b.Y, n, (int64_t)1, k, b.C, b.asg,
+                       (float *)nullptr, (float *)nullptr, b.hist);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(km_keys_kernel, dim3(g), dim3(256), 0, st, b.Y, b.asg, n, b.k1, b.vals);
     size_t tb = b.tmp_bytes;

@@ -120,11 +120,13 @@ MFMA_BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
 
 def run_c4(args):
     """BASELINE config 4: 2M x 128 L2-normalised embeddings, core distances over minPts = 16
-    (EXCL_SELF) on the MFMA path (K1m: bf16-split norm-expansion screen on MFMA + exact FP64
-    re-check of every pair the screen cannot exclude; lists bit-identical to the FP64 scan).
-    Timed region: pinned host X -> H2D -> core distances -> D2H of the cores.  One GPU (the
-    core distances of one partition; C4 names no sharding).  Roofline: the algorithmic
-    2 n^2 d flops of all-pairs dot products / the K1m kernel time vs the dense bf16 peak."""
+    (EXCL_SELF) on the MFMA path (K1m: k-means layout, bf16-split norm-expansion screen on MFMA
+    over the (query group, candidate block) pairs the FP64 balls cannot exclude, candidate log,
+    exact FP64 re-check of the log; lists bit-identical to the FP64 scan).  Timed region: pinned
+    host X -> H2D -> core distances -> D2H of the cores.  One GPU (the core distances of one
+    partition; C4 names no sharding).  Roofline of the screen kernel: the MFMA flops it issues
+    (3 bf16 products per pair of every computed block pair) / its time vs the dense bf16 peak;
+    the all-pairs-equivalent 2 n^2 d rate rides along."""
     import torch
     pkg = importlib.import_module(PKG)
     A = importlib.import_module(PKG + "._capi")
@@ -152,18 +154,24 @@ def run_c4(args):
         step()
     torch.cuda.synchronize()
     ctx.set_timing(True)
-    ctx.kernel_time("knn_mfma")
+    for name in ("knn_mfma", "knn_mfma_final", "knn_mfma_order"):
+        ctx.kernel_time(name)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     k_ms, k_calls = ctx.kernel_time("knn_mfma")
+    f_ms, _ = ctx.kernel_time("knn_mfma_final")
+    o_ms, _ = ctx.kernel_time("knn_mfma_order")
     ctx.set_timing(False)
-    k_s = k_ms / 1e3 / args.steps  # K1m kernel time of one step (HIP events on its stream)
-    n_pad = -(-n // 64) * 64
+    k_s = k_ms / 1e3 / args.steps  # K1m screen kernel time of one step (HIP events on its stream)
+    blocks = ctx.get_stat("knn_mfma_blocks")  # (query group, 32-candidate block) pairs of the last call
+    rows = ctx.get_stat("knn_mfma_group_rows")
+    DP = 32 if d <= 32 else 64 if d <= 64 else 128 if d <= 128 else 256
+    pairs = blocks * rows * 32
     alg = 2.0 * n * n * d
-    issued = 2 * 3 * 2.0 * n_pad * n_pad * d  # bound + exact pass, 3 bf16 products each (split operands)
+    issued = 3 * 2.0 * pairs * DP  # 3 bf16 products per computed pair (split operands)
     c = core_h.numpy()
     assert np.all(np.isfinite(c)) and np.all(c >= 0)
     line = {"metric": "points/sec end-to-end + mutual-reach distance evals/sec at 1/2/4/8 GPUs",
@@ -175,11 +183,13 @@ def run_c4(args):
                        "points": n, "d": d, "min_pts": mp,
                        "timed": "pinned host X -> H2D -> K1m core distances -> D2H of the cores"},
             "mrd_evals_per_s": n * (n - 1) / dt,
-            "roofline": {"bound": "mfma", "kernel": "knn_mfma (K1m)", "achieved": alg / k_s / 1e12,
-                         "peak": MFMA_BF16_DENSE_TFLOPS, "unit": "TFLOP/s", "frac": alg / k_s / 1e12 / MFMA_BF16_DENSE_TFLOPS,
-                         "traffic": None, "work": "algorithmic 2 n^2 d (all-pairs dot products)",
-                         "issued_mfma_tflops": issued / k_s / 1e12, "kernel_s_per_step": k_s,
-                         "launches_per_step": k_calls / args.steps}}
+            "roofline": {"bound": "mfma", "kernel": "knn_mfma_screen_kernel (K1m)", "achieved": issued / k_s / 1e12,
+                         "peak": MFMA_BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                         "frac": issued / k_s / 1e12 / MFMA_BF16_DENSE_TFLOPS, "traffic": None,
+                         "work": "issued: 3 bf16 MFMA products x 2 DP flops per computed (query, candidate) pair",
+                         "computed_pair_frac": pairs / (n * n), "all_pairs_equivalent_tflops": alg / k_s / 1e12,
+                         "kernel_s_per_step": k_s, "launches_per_step": k_calls / args.steps,
+                         "order_s_per_step": o_ms / 1e3 / args.steps, "recheck_s_per_step": f_ms / 1e3 / args.steps}}
     if not args.no_cpu_baseline:
         from oracle import oracle as O
         O.lib()
@@ -287,8 +297,8 @@ def run_partitioned(args, workload):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="default 10 (c2), 1 (c3/c4/c5)")
-    ap.add_argument("--warmup", type=int, default=None, help="default 3 (c2), 0 (c3/c5), 1 (c4)")
+    ap.add_argument("--steps", type=int, default=None, help="default 10 (c2), 5 (c4), 1 (c3/c5)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 3 (c2), 2 (c4), 0 (c3/c5)")
     ap.add_argument("--n", type=int, default=N_POINTS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
@@ -297,9 +307,9 @@ def main():
     ap.add_argument("--phases", action="store_true", help="c3/c5: per-phase times (synchronising)")
     args = ap.parse_args()
     if args.steps is None:
-        args.steps = 10 if args.workload == "c2" else 1
+        args.steps = {"c2": 10, "c4": 5}.get(args.workload, 1)
     if args.warmup is None:
-        args.warmup = {"c2": 3, "c4": 1}.get(args.workload, 0)
+        args.warmup = {"c2": 3, "c4": 2}.get(args.workload, 0)
     if args.workload == "c4":
         return run_c4(args)
     if args.workload != "c2":
