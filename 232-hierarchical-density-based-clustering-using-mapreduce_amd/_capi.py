@@ -150,6 +150,7 @@ class Context:
     """One hdb_ctx per (thread, device); owns a stream (or borrows torch's)."""
 
     _tls = threading.local()
+    _all: list = []  # every context created (diagnostic stat totals across threads)
 
     def __init__(self, device: int = 0):
         h = C.c_void_p()
@@ -157,6 +158,11 @@ class Context:
         self.h = h
         self.device = device
         self._stream = None
+        Context._all.append(self)
+
+    @classmethod
+    def stat_total(cls, name: str) -> int:
+        return sum(c.get_stat(name) for c in cls._all)
 
     @classmethod
     def get(cls, device: int = 0) -> "Context":

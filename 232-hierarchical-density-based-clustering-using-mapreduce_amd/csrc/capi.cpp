@@ -382,7 +382,7 @@ int hdb_local_model(hdb_ctx *ctx, const double *rep, const double *info, int64_t
                         mva.data(), mvb.data(), mw.data());
         }
         auto t2 = clk::now();
-        g_lm_us[0] = g_lm_us[1] = g_lm_us[2] = 0;
+        for (auto &v : g_lm_us) v = 0;
         std::vector<int32_t> lab(b);
         std::vector<int32_t> iva(ne), ivb(ne);
         std::vector<double> iw(ne);
@@ -394,6 +394,9 @@ int hdb_local_model(hdb_ctx *ctx, const double *rep, const double *info, int64_t
         ctx->stats["lm_quicksort_us"] += g_lm_us[0];
         ctx->stats["lm_tree_us"] += g_lm_us[1];
         ctx->stats["lm_fosc_us"] += g_lm_us[2];
+        ctx->stats["lm_fosc_select_us"] += g_lm_us[3];
+        ctx->stats["lm_fosc_label_us"] += g_lm_us[4];
+        ctx->stats["lm_fosc_noise_us"] += g_lm_us[5];
         ctx->stats["lm_calls"] += 1;
         if (rc) HDB_THROW(rc, "local model raised a reference exception");
         std::copy(lab.begin(), lab.end(), labels);

@@ -255,6 +255,10 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
         ctx->knn_mfma_two_pass = value != 0;
         return HDB_OK;
     }
+    if (k == "nearest_grouped") {
+        ctx->nearest_grouped = value != 0;
+        return HDB_OK;
+    }
     if (k == "knn_mfma_prune") {
         ctx->knn_mfma_prune = value != 0;
         return HDB_OK;

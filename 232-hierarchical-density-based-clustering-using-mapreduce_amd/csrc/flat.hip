@@ -641,7 +641,9 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         HIP_CHECK(rocprim::exclusive_scan(tmp, tb, keep, pos, 0, (size_t)ne, rocprim::plus<int32_t>(), st));
         hipLaunchKernelGGL(fl_compact, dim3(grid_for(ne)), dim3(256), 0, st, va, vb, w, ne, keep, pos, m, ca, cb, cw,
                            m_dev);
-        hipLaunchKernelGGL(fl_order, dim3(grid_for(ne) / 4 + 1), dim3(1024), 0, st, cw, m_dev, flags);
+        // a descending list sets bit 1 in every workgroup: few workgroups, few same-address atomics
+        hipLaunchKernelGGL(fl_order, dim3((unsigned)std::min<int64_t>(grid_for(ne) / 4 + 1, 256)), dim3(1024), 0, st,
+                           cw, m_dev, flags);
     }
     HIP_CHECK(hipMemcpyAsync(pin, words, sizeof(int64_t) * 3, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));

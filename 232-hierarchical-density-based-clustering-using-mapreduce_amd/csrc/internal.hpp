@@ -65,7 +65,7 @@ int flat_labels_host(const int32_t *va, const int32_t *vb, const double *w, int6
                      int32_t *labels, int64_t *n_clusters);
 int quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne);
 // host phase times of local_model_host (us): quicksort, cluster tree, FOSC + noise
-extern thread_local int64_t g_lm_us[3];
+extern thread_local int64_t g_lm_us[6];  // + FOSC parts: selection walk, labelling, noise
 int local_model_host(const double *rep, const double *eB, const double *nnB, const int32_t *nB, int64_t b, int d,
                      int32_t min_cl_size, int metric, int32_t *mva, int32_t *mvb, double *mw, int32_t *labels,
                      int32_t *ic_va, int32_t *ic_vb, double *ic_w, int64_t *n_ic);

@@ -579,6 +579,11 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
         get(par->label)->push_back(r);
     }
     // Collections.sort by birth level (stable)
+    using fclk = std::chrono::steady_clock;
+    auto fus = [](fclk::time_point a, fclk::time_point b) {
+        return (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
+    };
+    const auto f0 = fclk::now();
     std::vector<Cl *> sorted = tree;
     std::stable_sort(sorted.begin(), sorted.end(), [](const Cl *a, const Cl *b) { return a->birth < b->birth; });
     for (int64_t o = 0; o < b; o++) flat[o] = 0;
@@ -587,6 +592,10 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
     std::vector<uint32_t> vis(maxlab + 2, 0);  // generation stamps (one BFS per record)
     uint32_t vgen = 0;
     std::vector<int32_t> q;
+    // A node some earlier BFS visited has had its whole subtree walked: the walk only clears
+    // sol (never sets it), so walking that subtree again changes nothing -- it is not
+    // re-entered (the reference's repeated BFS is O(clusters^2) on deep trees).
+    std::vector<char> walked(maxlab + 2, 0);
     for (auto *c : sorted) {
         const int32_t key = c->label;
         auto *A = get(key);
@@ -601,19 +610,21 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
                         vgen = 1;
                     }
                     int32_t rootV = (int32_t)r.v[1];
+                    r.v[3] = 0.0;
+                    sol[rootV] = 0;
+                    if (rootV < 0 || rootV > maxlab + 1 || walked[rootV]) continue;
                     q.clear();
                     vis[rootV] = vgen;
                     q.push_back(rootV);
-                    r.v[3] = 0.0;
-                    sol[rootV] = 0;
                     for (size_t h = 0; h < q.size(); h++) {
                         int32_t v = q[h];
+                        walked[v] = 1;
                         auto *Av = get(v);
                         if (Av)
                             for (auto &rr : *Av) {
                                 sol[v] = 0;
                                 int32_t cc = (int32_t)rr.v[1];
-                                if (vis[cc] != vgen) {
+                                if (vis[cc] != vgen && !walked[cc]) {
                                     q.push_back(cc);
                                     vis[cc] = vgen;
                                 }
@@ -631,19 +642,60 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
             sol[key] = 0;
         }
     }
+    const auto f1 = fclk::now();
+    // The reference labels the selected clusters in birth order, a later one overwriting an
+    // earlier one's members (nested selections happen: the BFS above does not clear childless
+    // descendants).  Equivalently, in reverse order the first cluster to reach a point keeps
+    // it -- and a dendrogram subtree walked once is never re-entered, so the labelling is
+    // O(b) instead of O(b x nested selections).
     std::vector<int32_t> stk;
     for (auto *c : sorted)
-        if (sol[c->label]) {
-            if (c->node >= 0 && D) {
-                D->leaves(c->node, stk, [&](int32_t m) { flat[m] = c->label; });
-                continue;
-            }
-            for (int32_t m : c->members) {
+        if (sol[c->label] && !(c->node >= 0 && D))
+            for (int32_t m : c->members)
                 if (m < 0 || m >= b) return HDB_EREF_OOB;
+    std::vector<char> got((size_t)b, 0), claimed(D ? (size_t)(2 * b) : 0, 0);
+    for (auto it = sorted.rbegin(); it != sorted.rend(); ++it) {
+        const Cl *c = *it;
+        if (!sol[c->label]) continue;
+        if (c->node >= 0 && D) {
+            stk.assign(1, c->node);
+            while (!stk.empty()) {
+                const int32_t x = stk.back();
+                stk.pop_back();
+                if (claimed[x]) continue;
+                claimed[x] = 1;
+                if (x < b) {
+                    if (!got[x]) {
+                        got[x] = 1;
+                        flat[x] = c->label;
+                    }
+                    continue;
+                }
+                stk.push_back(D->r[x - b]);
+                stk.push_back(D->l[x - b]);
+            }
+            continue;
+        }
+        for (int32_t m : c->members)
+            if (!got[m]) {
+                got[m] = 1;
                 flat[m] = c->label;
             }
+    }
+    const auto f2 = fclk::now();
+    g_lm_us[3] += fus(f0, f1);
+    g_lm_us[4] += fus(f1, f2);
+    struct NoiseTimer {
+        fclk::time_point t = fclk::now();
+        ~NoiseTimer() {
+            g_lm_us[5] += (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(fclk::now() - t).count();
         }
-    // noise -> first later-valid neighbour in index order (:485-502)
+    } noise_timer;
+    // noise -> first later-valid neighbour in index order (:485-502).  With no labelled bubble
+    // at all the reference's double loop changes nothing: skip its b^2 scan.
+    bool any_label = false;
+    for (int64_t p = 0; p < b && !any_label; p++) any_label = flat[p] != 0;
+    if (!any_label) return HDB_OK;
     for (int64_t p = 0; p < b; p++) {
         double minD = JMAX;
         for (int64_t nb = 0; nb < b; nb++) {
@@ -663,7 +715,7 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
     return HDB_OK;
 }
 
-thread_local int64_t g_lm_us[3];
+thread_local int64_t g_lm_us[6];
 
 int local_model_host(const double *rep, const double *eB, const double *nnB, const int32_t *nB, int64_t b, int d,
                      int32_t min_cl_size, int metric, int32_t *mva, int32_t *mvb, double *mw, int32_t *labels,

@@ -13,7 +13,12 @@
 // the union of its lanes' ranges with per-lane masks; sorted points make it uniform).
 #include <hipcub/hipcub.hpp>
 
+#include <cmath>
+#include <numeric>
+#include <vector>
+
 #include "common.hpp"
+#include "sort.hpp"
 
 namespace hdb {
 
@@ -226,11 +231,294 @@ static void stable_sort_by_key(hdb_ctx *ctx, const int32_t *keys, int64_t n, int
                                                  ctx->stream));
 }
 
+// ------------------------------------------------------------------ K3g: grouped samples
+// Large unkeyed euclidean scans (the recursive-sampling levels of C3/C5: millions of points
+// against 4k-16k samples).  The samples are cut on the host into groups of G by recursive
+// median splits (widest dimension), each group with its FP64 bounding box; every point
+// descends the split tree to a "home" group, and the points are processed in home order so a
+// wave's lanes share their candidate groups.  A lane first scans its home group, then the wave
+// walks every group's box: a group is scanned (for all lanes) when some lane's box lower bound
+// could still reach its best value.  Exact: the box bound uses the reference's own summation
+// order on monotonically rounded gaps (every computed sample distance in the box is >= it), a
+// group is skipped only when that bound exceeds r^2 (1 + 2^-48) (no sample in it can reach the
+// best sqrt value r, ties included), and candidates are kept by (sqrt value, sample index)
+// lexicographically -- the reference's first minimum in sample order (FirstStep.java:74-85),
+// whatever order the groups are scanned in.
+struct NNg {
+    double r, g2;  // best sqrt value, pruning guard r^2 (1 + 2^-48)
+    int i;
+};
+
+__device__ __forceinline__ void nng_consider(NNg &b, double s, int j) {
+    if (s <= b.g2) {  // NaN never passes
+        const double r = sqrt(s);
+        if (r < b.r || (r == b.r && j < b.i)) {
+            b.r = r;
+            b.i = j;
+            b.g2 = r * r * (1.0 + 0x1p-48);
+        }
+    }
+}
+
+struct KdNode {
+    int dim;      // -1: leaf
+    double split;
+    int left, right;  // children (node ids); leaf: left = group id
+};
+
+// home group of every point: descend its key's split tree (keys: sorted distinct sample keys,
+// root/glo/ghi per key); a point whose key has no sample gets key slot -1 (Java's init)
+__global__ void nng_home_kernel(const double *__restrict__ X, int64_t n, int d, const KdNode *__restrict__ tree,
+                                const int32_t *__restrict__ xkey, const int32_t *__restrict__ keys, int nk,
+                                const int32_t *__restrict__ root, uint32_t *__restrict__ hkey,
+                                int32_t *__restrict__ val, int32_t *__restrict__ kslot) {
+    HDB_GRID_STRIDE(p, n) {
+        int ks = 0;
+        if (xkey) {
+            const int32_t k = xkey[p];
+            int a = 0, b = nk;
+            while (a < b) {
+                const int mid = (a + b) >> 1;
+                if (keys[mid] < k) a = mid + 1;
+                else b = mid;
+            }
+            ks = (a < nk && keys[a] == k) ? a : -1;
+        }
+        uint32_t g = 0xffffffffu;  // no sample: sorts last
+        if (ks >= 0) {
+            int v = root[ks];
+            while (tree[v].dim >= 0) v = X[p * d + tree[v].dim] < tree[v].split ? tree[v].left : tree[v].right;
+            g = (uint32_t)tree[v].left;
+        }
+        hkey[p] = g;
+        val[p] = (int32_t)p;
+        kslot[p] = ks;
+    }
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void nng_search_kernel(const double *__restrict__ X, int64_t n,
+                                                         const int32_t *__restrict__ order,
+                                                         const uint32_t *__restrict__ home,
+                                                         const double *__restrict__ Sg, const int32_t *__restrict__ sidx,
+                                                         const double *__restrict__ boxes, int ng,
+                                                         const int32_t *__restrict__ kslot,
+                                                         const int32_t *__restrict__ glo,
+                                                         const int32_t *__restrict__ ghi,
+                                                         int32_t *__restrict__ out_i, double *__restrict__ out_d) {
+    extern __shared__ double box_s[];  // ng x 2D (lo then hi), when it fits
+    const bool lds_boxes = ng * 2 * D * 8 <= 65536;
+    if (lds_boxes)
+        for (int k = threadIdx.x; k < ng * 2 * D; k += blockDim.x) box_s[k] = boxes[k];
+    __syncthreads();
+    const double *bx = lds_boxes ? box_s : boxes;
+    const int64_t pos = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t p = pos < n ? order[pos] : 0;
+    const int ks = pos < n ? kslot[p] : -1;
+    const bool live = ks >= 0;  // a point whose key has samples
+    double x[D];
+#pragma unroll
+    for (int c = 0; c < D; c++) x[c] = X[p * D + c];
+    NNg b{JMAX, INFINITY, -1};
+    const int hg = live ? (int)home[pos] : 0;
+    const int g_lo = live ? glo[ks] : ng, g_hi = live ? ghi[ks] : 0;  // the key's groups
+    int w_lo = g_lo, w_hi = g_hi;
+    for (int o = 32; o >= 1; o >>= 1) {
+        w_lo = min(w_lo, __shfl_xor(w_lo, o));
+        w_hi = max(w_hi, __shfl_xor(w_hi, o));
+    }
+    // home group first (per-lane addresses)
+    for (int k = 0; k < G && live; k++) {
+        const double *sr = Sg + ((int64_t)hg * G + k) * D;
+        double acc = sq_diff(x[0], sr[0]);
+#pragma unroll
+        for (int c = 1; c < D; c++) acc = acc + sq_diff(x[c], sr[c]);
+        nng_consider(b, acc, sidx[(int64_t)hg * G + k]);
+    }
+    // every group whose box can still reach the lane's best (wave-uniform loop)
+    for (int g = w_lo; g < w_hi; g++) {
+        const double *lo = bx + (int64_t)g * 2 * D, *hi = lo + D;
+        double gap0 = fmax(fmax(lo[0] - x[0], x[0] - hi[0]), 0.0);
+        double lb = gap0 * gap0;
+#pragma unroll
+        for (int c = 1; c < D; c++) {
+            const double gc = fmax(fmax(lo[c] - x[c], x[c] - hi[c]), 0.0);
+            lb = lb + gc * gc;
+        }
+        const bool need = live && g >= g_lo && g < g_hi && g != hg && lb <= b.g2;
+        if (!__ballot(need)) continue;
+        for (int k = 0; k < G; k++) {
+            const double *sr = Sg + ((int64_t)g * G + k) * D;  // uniform
+            double acc = sq_diff(x[0], sr[0]);
+#pragma unroll
+            for (int c = 1; c < D; c++) acc = acc + sq_diff(x[c], sr[c]);
+            if (need) nng_consider(b, acc, sidx[(int64_t)g * G + k]);
+        }
+    }
+    if (pos < n) {
+        out_i[p] = b.i < 0 ? 0 : b.i;  // no candidate below MAX: Java's initial nearest = 0
+        if (out_d) out_d[p] = b.i < 0 ? JMAX : b.r;
+    }
+}
+
+// host: median-split groups of the samples (per key when keyed); returns false when the path
+// does not apply
+static bool nearest_grouped(hdb_ctx *ctx, const double *X, int64_t n, const double *S, int64_t m, int d,
+                            const int32_t *xkey, const int32_t *skey, int32_t *out_i, double *out_d) {
+    if (!ctx->nearest_grouped || !(d == 2 || d == 3 || d == 4 || d == 8 || d == 16)) return false;
+    if (m < 1024 || n < 8192 || n > INT32_MAX) return false;
+    const int G = d <= 8 ? 32 : 64;
+    hipStream_t st = ctx->stream;
+    std::vector<double> hs((size_t)m * d);
+    std::vector<int32_t> hk(skey ? (size_t)m : 0);
+    HIP_CHECK(hipMemcpyAsync(hs.data(), S, sizeof(double) * hs.size(), hipMemcpyDeviceToHost, st));
+    if (skey) HIP_CHECK(hipMemcpyAsync(hk.data(), skey, 4 * (size_t)m, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    for (double v : hs)
+        if (!std::isfinite(v)) return false;  // the plain scan keeps the reference's NaN/inf behaviour
+    // samples of each key, in list order
+    std::vector<int32_t> idx((size_t)m);
+    std::iota(idx.begin(), idx.end(), 0);
+    if (skey) std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) { return hk[a] < hk[b]; });
+    std::vector<int32_t> keys, roots, glo, ghi;
+    std::vector<KdNode> tree;
+    std::vector<std::pair<int64_t, int64_t>> grp;  // [lo, hi) of idx per group
+    struct Task {
+        int64_t lo, hi;
+        int node;
+    };
+    std::vector<Task> stack;
+    for (int64_t k0 = 0; k0 < m;) {
+        int64_t k1 = k0 + 1;
+        while (skey && k1 < m && hk[idx[k1]] == hk[idx[k0]]) k1++;
+        if (!skey) k1 = m;
+        keys.push_back(skey ? hk[idx[k0]] : 0);
+        roots.push_back((int)tree.size());
+        glo.push_back((int)grp.size());
+        tree.push_back(KdNode{-1, 0.0, 0, 0});
+        stack.push_back({k0, k1, roots.back()});
+        while (!stack.empty()) {
+            const Task t = stack.back();
+            stack.pop_back();
+            if (t.hi - t.lo <= G) {
+                tree[t.node] = KdNode{-1, 0.0, (int)grp.size(), 0};
+                grp.push_back({t.lo, t.hi});
+                continue;
+            }
+            int dim = 0;
+            double best = -1;
+            for (int c = 0; c < d; c++) {
+                double lo = INFINITY, hi = -INFINITY;
+                for (int64_t k = t.lo; k < t.hi; k++) {
+                    const double v = hs[(size_t)idx[k] * d + c];
+                    lo = std::min(lo, v);
+                    hi = std::max(hi, v);
+                }
+                if (hi - lo > best) {
+                    best = hi - lo;
+                    dim = c;
+                }
+            }
+            // split at a multiple of G so every group of the node but the last is full
+            const int64_t cnt = t.hi - t.lo, halfg = (cnt / G + 1) / 2;
+            const int64_t mid = t.lo + std::max<int64_t>(1, halfg) * G;
+            std::nth_element(idx.begin() + t.lo, idx.begin() + mid, idx.begin() + t.hi, [&](int32_t a, int32_t b2) {
+                const double va = hs[(size_t)a * d + dim], vb = hs[(size_t)b2 * d + dim];
+                return va < vb || (va == vb && a < b2);
+            });
+            const int l = (int)tree.size(), r = l + 1;
+            tree.push_back(KdNode{-1, 0.0, 0, 0});
+            tree.push_back(KdNode{-1, 0.0, 0, 0});
+            tree[t.node] = KdNode{dim, hs[(size_t)idx[mid] * d + dim], l, r};
+            stack.push_back({mid, t.hi, r});
+            stack.push_back({t.lo, mid, l});
+        }
+        ghi.push_back((int)grp.size());
+        k0 = k1;
+    }
+    const int ng = (int)grp.size(), nk = (int)keys.size();
+    std::vector<double> hg((size_t)ng * G * d, NAN), hb((size_t)ng * 2 * d);
+    std::vector<int32_t> hi_((size_t)ng * G, -1);
+    for (int g = 0; g < ng; g++) {
+        for (int c = 0; c < d; c++) {
+            hb[(size_t)g * 2 * d + c] = INFINITY;
+            hb[(size_t)g * 2 * d + d + c] = -INFINITY;
+        }
+        for (int64_t k = grp[g].first; k < grp[g].second; k++) {
+            const int64_t slot = (int64_t)g * G + (k - grp[g].first);
+            hi_[slot] = idx[k];
+            for (int c = 0; c < d; c++) {
+                const double v = hs[(size_t)idx[k] * d + c];
+                hg[(size_t)slot * d + c] = v;
+                hb[(size_t)g * 2 * d + c] = std::min(hb[(size_t)g * 2 * d + c], v);
+                hb[(size_t)g * 2 * d + d + c] = std::max(hb[(size_t)g * 2 * d + d + c], v);
+            }
+        }
+    }
+    // device scratch (A_WORK1): groups, ids, boxes, tree, key tables, keys/order + sort
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+        size_t o = off;
+        off += (bytes + 255) & ~size_t(255);
+        return o;
+    };
+    size_t tb = 0;
+    HIP_CHECK(sort_pairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr, (const int32_t *)nullptr,
+                         (int32_t *)nullptr, n, 0, 32, st));
+    const size_t o_g = carve(sizeof(double) * hg.size()), o_i = carve(4 * hi_.size()), o_b = carve(8 * hb.size()),
+                 o_t = carve(sizeof(KdNode) * tree.size()), o_kt = carve(16 * (size_t)nk), o_k1 = carve(4 * (size_t)n),
+                 o_k2 = carve(4 * (size_t)n), o_v1 = carve(4 * (size_t)n), o_v2 = carve(4 * (size_t)n),
+                 o_ks = carve(4 * (size_t)n), o_tmp = carve(tb);
+    char *base = (char *)arena(ctx, A_WORK1, off);
+    double *dg = (double *)(base + o_g), *db = (double *)(base + o_b);
+    int32_t *di = (int32_t *)(base + o_i);
+    KdNode *dt = (KdNode *)(base + o_t);
+    int32_t *dkeys = (int32_t *)(base + o_kt), *droot = dkeys + nk, *dglo = droot + nk, *dghi = dglo + nk;
+    uint32_t *k1 = (uint32_t *)(base + o_k1), *k2 = (uint32_t *)(base + o_k2);
+    int32_t *v1 = (int32_t *)(base + o_v1), *v2 = (int32_t *)(base + o_v2), *kslot = (int32_t *)(base + o_ks);
+    std::vector<int32_t> ktab((size_t)4 * nk);
+    std::copy(keys.begin(), keys.end(), ktab.begin());
+    std::copy(roots.begin(), roots.end(), ktab.begin() + nk);
+    std::copy(glo.begin(), glo.end(), ktab.begin() + 2 * nk);
+    std::copy(ghi.begin(), ghi.end(), ktab.begin() + 3 * nk);
+    HIP_CHECK(hipMemcpyAsync(dg, hg.data(), sizeof(double) * hg.size(), hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(di, hi_.data(), 4 * hi_.size(), hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(db, hb.data(), 8 * hb.size(), hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(dt, tree.data(), sizeof(KdNode) * tree.size(), hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(dkeys, ktab.data(), 4 * ktab.size(), hipMemcpyHostToDevice, st));
+    KernelTimer t(ctx, "nearest_grouped");
+    const int g = (int)std::min<int64_t>(ceil_div(n, 256), 8192);
+    hipLaunchKernelGGL(nng_home_kernel, dim3(g), dim3(256), 0, st, X, n, d, dt, skey ? xkey : nullptr, dkeys, nk,
+                       droot, k1, v1, kslot);
+    HIP_CHECK(sort_pairs((void *)(base + o_tmp), tb, k1, k2, v1, v2, n, 0, 32, st));
+    const unsigned blocks = (unsigned)ceil_div(n, 256);
+    const size_t lds_arg = (size_t)ng * 2 * d * 8 <= 65536 ? (size_t)ng * 2 * d * 8 : 0;
+#define NNG_CASE(DD, GG)                                                                                         \
+    case DD:                                                                                                     \
+        hipLaunchKernelGGL((nng_search_kernel<DD, GG>), dim3(blocks), dim3(256), lds_arg, st, X, n, v2, k2, dg, \
+                           di, db, ng, kslot, dglo, dghi, out_i, out_d);                                         \
+        break;
+    switch (d) {
+        NNG_CASE(2, 32)
+        NNG_CASE(3, 32)
+        NNG_CASE(4, 32)
+        NNG_CASE(8, 32)
+        NNG_CASE(16, 64)
+    }
+#undef NNG_CASE
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(st));  // the host vectors above are read by the copies
+    return true;
+}
+
 void nearest_sample_device(hdb_ctx *ctx, const double *X, int64_t n, const double *S, int64_t m, int d,
                            int metric, const int32_t *xkey, const int32_t *skey, int32_t *out_i, double *out_d) {
     if (n == 0) return;
     if (n > INT32_MAX || m > INT32_MAX) HDB_THROW(HDB_EINVAL, "n or m exceeds int32");
     const bool keyed = xkey && skey;
+    if (metric == HDB_METRIC_EUCLIDEAN &&
+        nearest_grouped(ctx, X, n, S, m, d, keyed ? xkey : nullptr, keyed ? skey : nullptr, out_i, out_d))
+        return;
     // scratch carve
     size_t off = 0;
     auto carve = [&](size_t bytes) {

@@ -231,6 +231,7 @@ def run_partitioned(args, workload):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     pkg = importlib.import_module(PKG)
+    A = importlib.import_module(PKG + "._capi")
     cfg = PARTITIONED[workload]
     n = args.n if args.n != N_POINTS else cfg["n"]
     rng = np.random.default_rng(cfg["seed"])
@@ -288,6 +289,10 @@ def run_partitioned(args, workload):
                 "levels": len(lv), "leaves": int(sum(len(L["leaves"]) for L in lv)),
                 "model_errors": int(sum(len(L.get("model_errors", {})) for L in lv)),
                 "phases_s": {k: round(v, 4) for k, v in drv.timings.items()} if args.phases else None,
+                "local_model_s": ({k: round(A.Context.stat_total("lm_" + k + "_us") / 1e6, 3) for k in
+                                   ("core", "prim", "quicksort", "tree", "fosc", "fosc_select", "fosc_label",
+                                    "fosc_noise")} |
+                                  {"calls": A.Context.stat_total("lm_calls")}) if args.phases else None,
                 "roofline": None}
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -481,3 +481,66 @@ def test_prim_coop_slots_metrics_and_bubbles(pkg, oracle, d, metric, n):
     model = pkg.HdbscanDataBubbles()
     mst = model.constructMSTBubbles(X, nB, eB, nnB, ids, bcore, True)
     assert eq(mst.getVerticeA(), ra) and eq(mst.getVericeB(), rb) and eq(mst.getEges(), rw)
+
+
+# ------------------------------------------- K3g (grouped samples, box pruning) vs the scan
+@pytest.mark.parametrize("d", [2, 3, 4, 8, 16])
+def test_nearest_grouped_vs_oracle(pkg, oracle, d):
+    """The recursive-sampling shape (n >= 8192 points, m >= 1024 samples) takes K3g: median-split
+    sample groups scanned in home order with FP64 box pruning.  Rounded coordinates make exact
+    distance ties between samples common; the first minimum in sample order must survive."""
+    X = np.round(blobs(20000, d, 7, 40 + d), 1)
+    S = X[::13].copy()
+    assert S.shape[0] >= 1024
+    idx, dist = pkg.nearest_sample(X, S, with_dist=True)
+    r_idx, r_dist = oracle.nearest_sample(X, S)
+    assert eq(idx, r_idx) and eq(dist, r_dist)
+
+
+def test_nearest_grouped_sqrt_ties(pkg, oracle):
+    """Equal sqrt values from different squares, the larger square first in sample order, inside
+    a 2k-sample set: the grouped scan must keep the first (index 0), like Java."""
+    rng = np.random.default_rng(11)
+    c = rng.normal(size=(400000, 2))
+    c /= np.sqrt((c * c).sum(1))[:, None]
+    s = c[:, 0] * c[:, 0] + c[:, 1] * c[:, 1]
+    r = np.sqrt(s)
+    order = np.lexsort((s, r))
+    found = next((b, a) for a, b in zip(order[:-1], order[1:]) if r[a] == r[b] and s[a] < s[b])
+    far = 5.0 + rng.random((2046, 2))
+    S = np.concatenate([c[list(found)], far])
+    X = np.concatenate([np.zeros((5000, 2)), 5.0 + rng.random((5000, 2))])
+    idx, dist = pkg.nearest_sample(X, S, with_dist=True)
+    r_idx, r_dist = oracle.nearest_sample(X, S)
+    assert eq(idx, r_idx) and np.all(idx[:5000] == 0) and eq(dist, r_dist)
+
+
+def test_nearest_grouped_equals_scan_large(pkg):
+    """C5's level shape at 1/8 size: 2M x 8 points against 16,384 samples, K3g vs the plain scan."""
+    import torch
+    X = torch.from_numpy(blobs(2_000_000, 8, 100, 5)).cuda()
+    S = X[:: 2_000_000 // 16384][:16384].contiguous()
+    ctx = pkg.Context.get(0)
+    ctx.use_torch_stream()
+    try:
+        ctx.set_option("nearest_grouped", 1)
+        a_i, a_d = pkg.nearest_sample(X, S, ctx=ctx, with_dist=True)
+        ctx.set_option("nearest_grouped", 0)
+        b_i, b_d = pkg.nearest_sample(X, S, ctx=ctx, with_dist=True)
+    finally:
+        ctx.set_option("nearest_grouped", 1)
+    assert torch.equal(a_i, b_i) and torch.equal(a_d.view(torch.int64), b_d.view(torch.int64))
+
+
+def test_nearest_grouped_keyed(pkg, oracle):
+    """Keyed K3g (D3: the driver's one call over all big subsets): each key's samples get their
+    own split tree; a key without samples gives index 0 / MAX, as the Java init."""
+    rng = np.random.default_rng(9)
+    X = np.round(blobs(30000, 3, 9, 12), 1)
+    xk = rng.integers(0, 5, 30000).astype(np.int32)
+    S = X[::11].copy()
+    sk = xk[::11].copy()
+    sk[sk == 4] = 3  # key 4 has no samples
+    idx, dist = pkg.nearest_sample(X, S, None, xk, sk, with_dist=True)
+    r_idx, r_dist = oracle.nearest_sample(X, S, x_key=xk, s_key=sk)
+    assert eq(idx, r_idx) and eq(dist, r_dist)
