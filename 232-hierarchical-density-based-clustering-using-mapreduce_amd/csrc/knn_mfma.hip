@@ -355,12 +355,16 @@ struct LogEnt {
 constexpr int S_CST = 192;  // per 32-candidate block: hc[32], cn[32] (float), c2[32], cn[32] (double)
 
 #ifndef HDB_K1S_WAVES
-#define HDB_K1S_WAVES 4  // waves per workgroup (A/B knob: 8 = one workgroup of 512 queries per CU)
+#define HDB_K1S_WAVES 8  // waves per workgroup (A/B: 4 waves x 2 query tiles, 56.0 vs 51.9 ms at C4)
+#endif
+#ifndef HDB_K1S_QT
+#define HDB_K1S_QT 1  // query tiles per wave at DP <= 128 (64 fragment VGPRs: 4 waves per SIMD)
 #endif
 constexpr int NW = HDB_K1S_WAVES;
+constexpr int K1S_WPE = HDB_K1S_QT == 1 ? 4 : 2;  // waves per SIMD the VGPR budget allows
 template <int DP>
 struct ScreenCfg {
-    static constexpr int QT = DP <= 128 ? 2 : 1;  // query tiles per wave (VGPR-resident fragments)
+    static constexpr int QT = DP <= 128 ? HDB_K1S_QT : 1;  // query tiles per wave (VGPR-resident fragments)
     static constexpr int SQ = NW * 32 * QT;       // queries per workgroup
     static constexpr int CH = DP / 8;             // 16-B chunks per bf16 row
     static constexpr int BUF = 2 * 32 * DP;       // bf16 elements per staged block (hi rows, lo rows)
@@ -585,7 +589,7 @@ struct SbArgs {
 };
 
 template <int DP, int KC>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2))) void knn_mfma_screen_kernel(
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE, K1S_WPE))) void knn_mfma_screen_kernel(
     const __bf16 *__restrict__ Xh, const __bf16 *__restrict__ Xl, const double *__restrict__ nrm2,
     const double *__restrict__ nrm, const float *__restrict__ cst, int64_t n, int64_t n_pad, int excl,
     LogEnt *__restrict__ logs, int *__restrict__ log_cnt, float *__restrict__ thr_out, int *__restrict__ overflow,
@@ -611,7 +615,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __shared__ double qn2_s[SQ], qn_s[SQ];
 
     __shared__ float sk_s[NSB_MAX];           // superblock keys (lower bound - 2 max bound), ascending
-    __shared__ unsigned short si_s[NSB_MAX];  // superblock ids in key order
+    __shared__ unsigned short si_s[NSB_MAX];  // superblock ids in key order, then their block counts
+    __shared__ int sbs_s[NSB_MAX];            // first block of the i-th superblock in key order
     __shared__ float tmax_s[2][NW];           // per-wave max thr, written in alternate iterations
 
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, half = lane >> 5, col = lane & 31;
@@ -690,13 +695,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 
     bf16x8 bh[QT][NS], bl[QT][NS];
     float g[QT], qh[QT], a[QT];
-    int qloc[QT];
-    bool qv[QT];  // a real row (not padding)
+    // query t of this lane: row qbase + qloc(t) (recomputed: fewer live registers)
+    auto qloc_of = [&](int t) { return wave * 32 * QT + 32 * t + col; };
+    unsigned qvm = 0;  // bit t: a real row (not padding)
 #pragma unroll
     for (int t = 0; t < QT; t++) {
-        qloc[t] = wave * 32 * QT + 32 * t + col;
-        const int64_t row = qbase + qloc[t];
-        qv[t] = sb.perm[row] >= 0;
+        const int64_t row = qbase + qloc_of(t);
+        if (sb.perm[row] >= 0) qvm |= 1u << t;
 #pragma unroll
         for (int s = 0; s < NS; s++) {
             const int64_t o = row * DP + KS * s + 8 * half;
@@ -713,40 +718,44 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // instructions per block (CH/2 per array), CH/NW per wave; each lane's source offset inside
     // the block is fixed (swizzle on the source address, the LDS image stays lane-linear).
     constexpr int GW = (CH + NW - 1) / NW;  // wave-instructions per wave per block
-    uint32_t goff[GW];
-#pragma unroll
-    for (int k = 0; k < GW; k++) {
-        const int i = (wave + NW * k) % CH, ii = i >= CH / 2 ? i - CH / 2 : i;
-        const int p = ii * 64 + lane, row = p / CH, pc = p % CH, lc = pc ^ (row & (CH - 1));
-        goff[k] = (uint32_t)(row * DP + lc * 8);
-    }
-    auto stage = [&](auto B, int64_t cb) {
+    // buffer loads with a per-block SGPR resource and a 32-bit lane offset (no 64-bit
+    // per-lane address registers)
+    auto stage = [&](auto B, int64_t cb) __attribute__((always_inline)) {
         __bf16 *base = cbuf(B);
+        int lr = lane;
+        asm volatile("" : "+v"(lr));  // recomputed, not held live across the loop
+        const __amdgpu_buffer_rsrc_t rh =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(Xh + cb * DP), (short)0, 32 * DP * 2, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rl =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(Xl + cb * DP), (short)0, 32 * DP * 2, 0x00020000);
 #pragma unroll
         for (int k = 0; k < GW; k++) {
             const int i = wave + NW * k;
             if (CH % NW != 0 && i >= CH) break;  // wave-uniform
             const int arr = i >= CH / 2, ii = arr ? i - CH / 2 : i;
-            const __bf16 *src = (arr ? Xl : Xh) + cb * DP;  // uniform
-            __builtin_amdgcn_global_load_lds((const void *)(src + goff[k]),
-                                             (lds_ptr_t)(base + arr * 32 * DP + ii * 512), 16, 0, 0);
+            const int p = ii * 64 + lr, row = p / CH, pc = p % CH, lc = pc ^ (row & (CH - 1));
+            const int boff = (row * DP + lc * 8) * 2;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(arr ? rl : rh, (lds_ptr_t)(base + arr * 32 * DP + ii * 512), 16,
+                                                     boff, 0, 0, 0);
         }
-        if (wave == 0 && lane < S_CST / 4)
-            __builtin_amdgcn_global_load_lds((const void *)(cst + (cb >> 5) * S_CST + lane * 4),
-                                             (lds_ptr_t)cstb(B), 16, 0, 0);
+        if (wave == 0 && lane < S_CST / 4) {
+            const __amdgpu_buffer_rsrc_t rc =
+                __builtin_amdgcn_make_buffer_rsrc((void *)(cst + (cb >> 5) * S_CST), (short)0, S_CST * 4, 0x00020000);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (lds_ptr_t)cstb(B), 16, lane * 16, 0, 0, 0);
+        }
     };
 
     // the block sequence: superblocks in key order while key <= max thr of the group (read
     // one iteration late from alternating slots, so every wave takes the same decision)
     auto sb_blocks = [&](int i) -> int {
-        return sb.sb_nblk[si_s[i]];
+        return si_s[i];
     };
     float wmax = INFINITY;  // this wave's max thr over its real queries (uniform)
     int par = 0;
     int ci_sb = 0, ci_b = 0;  // current superblock (key order) and block within it; -1: done
     int64_t nproc = 0;
     auto step = [&](auto B, auto Bn) {
-        const int64_t cb = ((int64_t)sb.sb_blk[si_s[ci_sb]] + ci_b) * 32;
+        const int64_t cb = ((int64_t)sbs_s[ci_sb] + ci_b) * 32;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // block landed everywhere; the other buffer is free
         float thrmax = tmax_s[par ^ 1][0];
@@ -758,11 +767,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
             nx_b = 0;
             if (!(nx_sb < sb.nsb && sk_s[nx_sb] <= thrmax)) nx_sb = -1;
         }
-        if (nx_sb >= 0) stage(Bn, ((int64_t)sb.sb_blk[si_s[nx_sb]] + nx_b) * 32);
+        if (nx_sb >= 0) stage(Bn, ((int64_t)sbs_s[nx_sb] + nx_b) * 32);
         float *const cst_s = cstb(B);
         nproc++;
 
         const __bf16 *hb = cbuf(B), *lb = hb + 32 * DP;
+        // per-step LDS offsets recomputed each block (an opaque copy of the lane id keeps the
+        // compiler from hoisting eight live address registers out of the loop: VGPR pressure)
+        int colr = col;
+        asm volatile("" : "+v"(colr));
         f32x16 acc[QT];
 #pragma unroll
         for (int t = 0; t < QT; t++)
@@ -770,9 +783,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
             for (int r = 0; r < 16; r++) acc[t][r] = 0.f;
 #pragma unroll
         for (int s = 0; s < NS; s++) {
-            const int pc = (2 * s + half) ^ (col & (CH - 1));
-            const bf16x8 ah = *(const bf16x8 *)(hb + col * DP + pc * 8);
-            const bf16x8 al = *(const bf16x8 *)(lb + col * DP + pc * 8);
+            const int pc = (2 * s + half) ^ (colr & (CH - 1));
+            const bf16x8 ah = *(const bf16x8 *)(hb + colr * DP + pc * 8);
+            const bf16x8 al = *(const bf16x8 *)(lb + colr * DP + pc * 8);
 #pragma unroll
             for (int t = 0; t < QT; t++) {
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[t][s], acc[t], 0, 0, 0);
@@ -807,7 +820,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
             for (int t = 0; t < QT; t++) {
                 hm[t] = 0u;
-                if (m[t] >= a[t] && qv[t]) {
+                if (m[t] >= a[t] && ((qvm >> t) & 1u)) {
 #pragma unroll
                     for (int gi = 0; gi < 4; gi++) {
                         const float4 h4 = hc4[2 * gi + half], c4 = cn4[2 * gi + half];
@@ -822,7 +835,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 if (half == h) {
 #pragma unroll
                     for (int t = 0; t < QT; t++) {
-                        const int ql = qloc[t];
+                        const int ql = qloc_of(t);
                         const int64_t qid = qbase + ql;
                         const double q2 = qn2_s[ql], qn = qn_s[ql];
                         float *tp = top_s + ql * KC;
@@ -868,12 +881,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
             float wm = -INFINITY;
 #pragma unroll
             for (int t = 0; t < QT; t++) {
-                const float th = top_s[qloc[t] * KC + KC - 1];
+                const float th = top_s[qloc_of(t) * KC + KC - 1];
                 a[t] = qh[t] - 0.5f * th;
-                if (qv[t]) wm = fmaxf(wm, th);
+                if ((qvm >> t) & 1u) wm = fmaxf(wm, th);
             }
             for (int o = 32; o >= 1; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o));
-            wmax = wm;
+            wmax = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wm)));  // uniform
         }
         if (lane == 0) tmax_s[par][wave] = wmax;
         par ^= 1;
@@ -883,7 +896,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
     __syncthreads();
-    stage(B0{}, (int64_t)sb.sb_blk[si_s[0]] * 32);
+    // the key order's block ranges in LDS (no dependent global loads in the block loop)
+    for (int i = tid; i < sb.nsb; i += 64 * NW) {
+        const int id = si_s[i];
+        sbs_s[i] = sb.sb_blk[id];
+        si_s[i] = (unsigned short)sb.sb_nblk[id];
+    }
+    __syncthreads();
+    stage(B0{}, (int64_t)sbs_s[0] * 32);
     while (true) {
         step(B0{}, B1{});
         if (ci_sb < 0) break;
@@ -905,6 +925,29 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 
 // exact FP64 re-check of each query's logged candidates with lb <= thr (one wave per query),
 // then the KC smallest over the wave: the same values, in the same order, as the FP64 scan
+// exact squared distance in the reference's order with the query row in LDS and the candidate
+// row streamed in 16-double chunks, the next chunk in flight while the current one is summed
+__device__ __forceinline__ double exact_sq_pf(const double *a_lds, const double *__restrict__ b, int d) {
+    constexpr int U = 16;
+    double nb[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) nb[u] = b[u < d ? u : d - 1];
+    double sx = 0.0;
+    for (int j0 = 0; j0 < d; j0 += U) {
+        double cb[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) cb[u] = nb[u];
+        if (j0 + U < d) {
+#pragma unroll
+            for (int u = 0; u < U; u++) nb[u] = b[j0 + U + u < d ? j0 + U + u : d - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (j0 + u < d) sx = sx + sq_diff(a_lds[j0 + u], cb[u]);
+    }
+    return sx;
+}
+
 template <int KC>
 __global__ __launch_bounds__(256) void knn_mfma_final_kernel(const double *__restrict__ X, int64_t n, int d,
                                                              const LogEnt *__restrict__ logs,
@@ -918,12 +961,15 @@ __global__ __launch_bounds__(256) void knn_mfma_final_kernel(const double *__res
     const int cnt = log_cnt[q];
     const float t = thr[q];
     const int64_t qo = perm[q];  // the query's row in X (the lists follow X's order)
+    __shared__ double qrow_s[4][256];  // each wave's query row (d <= 256)
+    double *qr = qrow_s[threadIdx.x >> 6];
+    for (int c = lane; c < d; c += 64) qr[c] = X[qo * d + c];
     double top[KC];
 #pragma unroll
     for (int k = 0; k < KC; k++) top[k] = INFINITY;
     for (int j = lane; j < cnt; j += 64) {
         const LogEnt e = logs[q * S_LOGCAP + j];
-        if (e.lb <= t) topk_insert<KC>(top, exact_sq<0>(X + qo * d, X + (int64_t)perm[e.cid] * d, d));
+        if (e.lb <= t) topk_insert<KC>(top, exact_sq_pf(qr, X + (int64_t)perm[e.cid] * d, d));
     }
     for (int k = 0; k < KC; k++) {
         double mn = top[0];
