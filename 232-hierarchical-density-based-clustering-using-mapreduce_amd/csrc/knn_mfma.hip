@@ -361,7 +361,11 @@ constexpr int S_CST = 192;  // per 32-candidate block: hc[32], cn[32] (float), c
 #define HDB_K1S_QT 1  // query tiles per wave at DP <= 128 (64 fragment VGPRs: 4 waves per SIMD)
 #endif
 constexpr int NW = HDB_K1S_WAVES;
-constexpr int K1S_WPE = HDB_K1S_QT == 1 ? 4 : 2;  // waves per SIMD the VGPR budget allows
+#ifndef HDB_K1S_WPE
+#define HDB_K1S_WPE (HDB_K1S_QT == 1 ? 4 : 2)
+#endif
+constexpr int K1S_WPE = HDB_K1S_WPE;  // waves per SIMD (A/B at C4: 4 = two workgroups per CU, 51.7 ms, despite
+                                      // spilling some fragments; 3 = 168 VGPRs without spills, one workgroup, 57.0 ms)
 template <int DP>
 struct ScreenCfg {
     static constexpr int QT = DP <= 128 ? HDB_K1S_QT : 1;  // query tiles per wave (VGPR-resident fragments)
