@@ -275,6 +275,10 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
         ctx->knn_tree_min_n = value;
         return HDB_OK;
     }
+    if (k == "prim_coop_plain") {
+        ctx->prim_coop_plain = value != 0;
+        return HDB_OK;
+    }
     if (k == "prim_coop") {
         ctx->prim_coop = value != 0;
         return HDB_OK;

@@ -1079,15 +1079,31 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
     int32_t *pva = va + eo, *pvb = vb + eo;
     double *pw = w + eo;
     void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &gkey, &grow, &err};
-    {
-        KernelTimer t(ctx, "prim_coop");
-        HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_coop4_kernel<BS, DM, FULL>, dim3(nwg), dim3(BS), args, 0,
-                                             ctx->stream));
-    }
+    // A plain launch first: ROCm serialises cooperative launches device-wide, so the concurrent
+    // local models of one level (driver model pool) would queue behind each other.  The grid
+    // (<= 64 workgroups) is far below the device's capacity, and every inter-workgroup wait has
+    // a timeout: if the workgroups were not co-resident the kernel reports it and exits, the
+    // state is reset and the cooperative launch (guaranteed co-residency) runs instead.
     int h_err = 0;
-    HIP_CHECK(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    if (h_err) HDB_THROW(HDB_EDEVICE, "prim_coop: key sweep timed out (workgroups not co-resident)");
+    for (int attempt = ctx->prim_coop_plain ? 0 : 1; attempt < 2; attempt++) {
+        if (attempt == 1 && h_err) HIP_CHECK(hipMemsetAsync(base, 0, kbytes + rbytes + 256, ctx->stream));
+        {
+            KernelTimer t(ctx, "prim_coop");
+            if (attempt == 0)
+                hipLaunchKernelGGL((prim_coop4_kernel<BS, DM, FULL>), dim3(nwg), dim3(BS), 0, ctx->stream, L, nn,
+                                   self_edges, pva, pvb, pw, gkey, grow, err);
+            else
+                HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_coop4_kernel<BS, DM, FULL>, dim3(nwg), dim3(BS),
+                                                     args, 0, ctx->stream));
+            HIP_CHECK(hipGetLastError());
+        }
+        h_err = 0;
+        HIP_CHECK(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        if (!h_err) return true;
+        if (attempt == 0) ctx->stats["prim_coop_plain_retries"] += 1;
+    }
+    HDB_THROW(HDB_EDEVICE, "prim_coop: key sweep timed out (workgroups not co-resident)");
     return true;
 }
 

@@ -42,3 +42,35 @@ dt = (time.perf_counter() - t0) / reps
 res = {k: (ctx.get_stat(k) - base[k]) / reps / 1e3 for k in keys[:-1]}
 print(json.dumps({"b": b, "d": d, "rc": rcs[-1], "ms_per_model": dt * 1e3, "phases_ms": res,
                   "clusters": int(labels.max())}))
+
+# concurrency: T threads each running `reps` models on their own context (driver's model pool)
+import threading  # noqa: E402
+
+for T in (1, 2, 4):
+    ctxs = []
+
+    def worker():
+        c = pkg.Context.get(0)
+        ctxs.append(c)
+        o = {k: np.zeros(ne, t) for k, t in (("va", np.int32), ("vb", np.int32), ("w", np.float64),
+                                              ("iva", np.int32), ("ivb", np.int32), ("iw", np.float64))}
+        lab = np.zeros(b, np.int32)
+        nn = np.zeros(1, np.int64)
+        for _ in range(reps):
+            A.lib().hdb_local_model(c.h, A.ptr(rep), A.ptr(info), b, d, 4, 4, A.METRIC["euclidean"], A.ptr(lab),
+                                    A.ptr(o["va"]), A.ptr(o["vb"]), A.ptr(o["w"]), A.ptr(o["iva"]), A.ptr(o["ivb"]),
+                                    A.ptr(o["iw"]), A.ptr(nn))
+
+    base_p = pkg.Context.stat_total("lm_prim_us") if hasattr(pkg.Context, "stat_total") else 0
+    base_c = pkg.Context.stat_total("lm_core_us") if hasattr(pkg.Context, "stat_total") else 0
+    th = [threading.Thread(target=worker) for _ in range(T)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t0
+    prim = (pkg.Context.stat_total("lm_prim_us") - base_p) / (T * reps) / 1e3
+    core = (pkg.Context.stat_total("lm_core_us") - base_c) / (T * reps) / 1e3
+    print(json.dumps({"threads": T, "models": T * reps, "wall_s": wall, "prim_ms_per_model": prim,
+                      "core_ms_per_model": core}))
