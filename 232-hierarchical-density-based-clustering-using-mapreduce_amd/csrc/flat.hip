@@ -210,7 +210,7 @@ struct DC {
     int32_t *lab;       // 2m endpoint labels (vertex id < n, or n + root edge rank)
     LRec *lr;           // n + m label records
     int32_t *stamp;     // n + m: 2j = a label of an L edge at depth j
-    int32_t *hooked;    // m: the label an L edge's union hooked (-1: none)
+    int32_t *hooked;    // m: the label an L edge's union hooked (-1: none); dc_root then stores its representative
     int32_t *parent;    // m: parent edge rank (NONE: root)
     int32_t *esize;     // m: |C(e)|
     int32_t *eminid;    // m: smallest point id in C(e)
@@ -277,6 +277,7 @@ __global__ __launch_bounds__(ROOT_TB) void dc_root(DC c, int b, int j, int64_t n
             // the label this edge hooked is counted once, here; the final root label is
             // added by its root edge in dc_link
             const int32_t x = c.hooked[r];
+            c.hooked[r] = rep;  // dc_link reads the representative back instead of a second find
             const int32_t sz = x < 0 ? 0 : (x < c.n ? 1 : c.esize[x - c.n]);
             const int32_t mi = x < 0 ? NONE : (x < c.n ? x : c.eminid[x - c.n]);
             uint32_t h = uf_prio(rep, 0) & (ROOT_SLOTS - 1);
@@ -305,8 +306,8 @@ __global__ void dc_link(DC c, int b, int j, int64_t nl) {
     HDB_GRID_STRIDE(i, nl) {
         int64_t r = l_rank(i, b);
         if (r >= c.m) continue;
-        {  // L edge: a component root records |C(e)| and its smallest id
-            const int32_t rep = uf_find(c.lr, c.lab[2 * r]);
+        {  // L edge: a component root records |C(e)| and its smallest id (rep from dc_root)
+            const int32_t rep = c.hooked[r];
             const LRec q = c.lr[rep];
             if (q.rootedge == (int32_t)r) {
                 c.esize[r] = q.csize + (rep < c.n ? 1 : c.esize[rep - c.n]);
@@ -799,17 +800,24 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     for (int32_t c = 0; c < K - 1; c++) kids[fillp[hpar[c]]++] = c;
     contrib.resize((size_t)K);
     flg.assign((size_t)K, 0);
+    const int32_t *kp = kids.data();
+    double *cp = contrib.data();
     for (int32_t c = 0; c < K - 1; c++) {
         const int32_t k0 = koff[c], k1 = koff[c + 1];
-        if (k1 - k0 > 1)
-            std::sort(kids.begin() + k0, kids.begin() + k1, [&](int32_t a, int32_t b) { return hmin[a] < hmin[b]; });
         double prop = 0.0;
-        for (int32_t k = k0; k < k1; k++) prop = prop + contrib[kids[k]];
+        if (k1 - k0 == 2) {  // the common binary split: children summed in ascending smallest id
+            const int32_t a = kp[k0], b = kp[k0 + 1];
+            prop = hmin[a] < hmin[b] ? cp[a] + cp[b] : cp[b] + cp[a];
+        } else {
+            if (k1 - k0 > 2)
+                std::sort(kids.begin() + k0, kids.begin() + k1, [&](int32_t a, int32_t b) { return hmin[a] < hmin[b]; });
+            for (int32_t k = k0; k < k1; k++) prop = prop + cp[kp[k]];
+        }
         if (k1 == k0 || hstab[c] >= prop) {  // Cluster.propagate: ties keep the parent
-            contrib[c] = hstab[c];
+            cp[c] = hstab[c];
             flg[c] = 1;
         } else {
-            contrib[c] = prop;
+            cp[c] = prop;
         }
     }
     // selected = self-selected with no selected ancestor below the root (top-down = descending id)
