@@ -361,6 +361,19 @@ constexpr int S_CST = 192;  // per 32-candidate block: hc[32], cn[32] (float), c
 #define HDB_K1S_QT 1  // query tiles per wave at DP <= 128 (64 fragment VGPRs: 4 waves per SIMD)
 #endif
 constexpr int NW = HDB_K1S_WAVES;
+#ifndef HDB_K1S_XCD
+#define HDB_K1S_XCD 1  // contiguous query-group ranges per XCD (A/B at C4: screen 51.8 -> 50.7 ms)
+#endif
+#ifndef HDB_K1F_XCD
+#define HDB_K1F_XCD 0  // the same for the re-check's query blocks
+#endif
+#define K1S_XCD HDB_K1S_XCD
+// Workgroups are dealt round-robin over the 8 XCDs (block b runs on XCD b mod 8); this maps
+// them so XCD x takes one contiguous range of logical blocks (a bijection on [0, G)).
+__device__ __forceinline__ int64_t xcd_contig(int64_t b, int64_t G) {
+    const int64_t q = G >> 3, r = G & 7, x = b & 7, k = b >> 3;
+    return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+}
 #ifndef HDB_K1S_WPE
 #define HDB_K1S_WPE (HDB_K1S_QT == 1 ? 4 : 2)
 #endif
@@ -624,7 +637,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     __shared__ float tmax_s[2][NW];           // per-wave max thr, written in alternate iterations
 
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, half = lane >> 5, col = lane & 31;
-    const int64_t qbase = (int64_t)blockIdx.x * SQ;
+#if K1S_XCD
+    // query groups of one k-means cluster are consecutive and visit the same candidate
+    // superblocks: give each XCD (workgroups are dealt round-robin over the 8) a contiguous
+    // range of groups, so those candidates are fetched into one L2 instead of eight
+    const int64_t gid = xcd_contig(blockIdx.x, gridDim.x);
+#else
+    const int64_t gid = blockIdx.x;
+#endif
+    const int64_t qbase = gid * SQ;
     {
         // a group of padding rows only (uniform: every thread reads the same rows)
         bool any = false;
@@ -650,8 +671,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     int nsbp = 1;
     while (nsbp < sb.nsb) nsbp <<= 1;
     if (sb.prune) {
-        const double *mq = sb.qctr + (int64_t)blockIdx.x * DP;
-        const double RQ = sb.qrn[2 * blockIdx.x], NQ = sb.qrn[2 * blockIdx.x + 1];
+        const double *mq = sb.qctr + gid * DP;
+        const double RQ = sb.qrn[2 * gid], NQ = sb.qrn[2 * gid + 1];
         for (int i = tid; i < nsbp; i += 64 * NW) {
             float key = INFINITY;
             if (i < sb.nsb) {
@@ -960,7 +981,11 @@ __global__ __launch_bounds__(256) void knn_mfma_final_kernel(const double *__res
                                                              const int *__restrict__ perm,
                                                              double *__restrict__ lists) {
     const int lane = threadIdx.x & 63;
+#if HDB_K1F_XCD
+    const int64_t q = ((xcd_contig(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) >> 6);
+#else
     const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+#endif
     if (q >= n || perm[q] < 0) return;  // n: layout rows here
     const int cnt = log_cnt[q];
     const float t = thr[q];

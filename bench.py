@@ -116,6 +116,17 @@ def cpu_baseline(X, budget_s=10.0):
 
 C4 = dict(n=2_000_000, d=128, centers=200, noise=0.1, seed=4, min_pts=16)
 MFMA_BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
+# HBM bytes per launch from the PMC passes of this build (FETCH_SIZE / WRITE_SIZE runs of their
+# own, corrected by tools/pmc_summary.py): tools/profile_bench.sh (C2), tools/profile_c4.sh (C4)
+PMC_C2 = os.path.join(ROOT, "profiles", "r02", "final", "prof_c2", "pmc_summary.json")
+PMC_C4 = os.path.join(ROOT, "profiles", "r02", "c4_final", "pmc_summary.json")
+
+
+def _pmc_bytes(path, kernel):
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        return json.load(fh).get(kernel, {}).get("hbm_bytes_per_launch")
 
 
 def run_c4(args):
@@ -185,7 +196,11 @@ def run_c4(args):
             "mrd_evals_per_s": n * (n - 1) / dt,
             "roofline": {"bound": "mfma", "kernel": "knn_mfma_screen_kernel (K1m)", "achieved": issued / k_s / 1e12,
                          "peak": MFMA_BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
-                         "frac": issued / k_s / 1e12 / MFMA_BF16_DENSE_TFLOPS, "traffic": None,
+                         "frac": issued / k_s / 1e12 / MFMA_BF16_DENSE_TFLOPS,
+                         "traffic": _pmc_bytes(PMC_C4, "knn_mfma_screen_kernel"),
+                         "traffic_source": os.path.relpath(PMC_C4, ROOT),
+                         "hbm": {"achieved_gbs": (_pmc_bytes(PMC_C4, "knn_mfma_screen_kernel") or 0.0)
+                                 / (k_s / max(k_calls / args.steps, 1)) / 1e9, "peak": 8000.0},
                          "work": "issued: 3 bf16 MFMA products x 2 DP flops per computed (query, candidate) pair",
                          "computed_pair_frac": pairs / (n * n), "all_pairs_equivalent_tflops": alg / k_s / 1e12,
                          "kernel_s_per_step": k_s, "launches_per_step": k_calls / args.steps,
@@ -467,10 +482,7 @@ def main():
     achieved = visits / scan_s_step if scan_s_step > 0 else 0.0
     peak = visits / t_min if t_min > 0 else 0.0
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if os.path.exists(pmc):  # HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, tools/profile_bench.sh)
-        with open(pmc) as fh:
-            traffic = json.load(fh).get("boruvka_bvh_kernel", {}).get("hbm_bytes_per_launch")
+    traffic = _pmc_bytes(PMC_C2, "boruvka_bvh_kernel")
     fp64_tflops = 3 * D * (bor_evals / max(scan_n / tsteps, 1)) / avg_scan_s / 1e12 if avg_scan_s > 0 else 0.0
     evals = world * (n * n + n * (n - 1) / 2)  # kNN n^2 + MST n(n-1)/2
     line = {
@@ -501,7 +513,7 @@ def main():
                                          "algorithmic": n * n + n * (n - 1) // 2},
         "roofline": {"bound": "latency", "kernel": "boruvka_scan (boruvka_bvh_kernel)",
                      "unit": "node visits/s", "achieved": achieved, "peak": peak,
-                     "frac": achieved / peak if peak else 0.0, "traffic": traffic,
+                     "frac": achieved / peak if peak else 0.0, "traffic": traffic, "traffic_source": os.path.relpath(PMC_C2, ROOT),
                      "model": f"per round: visits x {MALL_HIT_NS:.0f} ns (one dependent Infinity-Cache "
                               f"round trip per visit) / min(waves, {WAVE_SLOTS} resident wave slots)",
                      "visits_per_step": visits, "rounds": [[v, w] for v, w in rounds],
