@@ -1116,26 +1116,44 @@ __global__ __launch_bounds__(256) void round_seed_kernel(const Rec<D> *__restric
                     }
                 }
             }
-            if (K > 0) {
+            if constexpr (K > 0) {
                 const Rec<D> &me = recs[i];
                 const double mcore = me.core;
                 const int32_t mid = me.id;
                 double sK = -INFINITY;
                 bool full = true;
+                // every neighbour's component, core and id loaded up front (unconditional,
+                // clamped to the point itself): K independent random loads in flight at once
+                // instead of K dependent rounds
+                int32_t nj[K], ncomp[K], nid[K];
+                double ns[K], ncore[K];
+#pragma unroll
                 for (int k = 0; k < K; k++) {
-                    const int32_t j = nb_pos[i * K + k];
-                    const double s = nb_s[i * K + k];
+                    nj[k] = nb_pos[i * K + k];
+                    ns[k] = nb_s[i * K + k];
+                }
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    const int64_t jc = nj[k] < 0 ? i : nj[k];
+                    ncomp[k] = pcomp[jc];
+                    ncore[k] = recs[jc].core;
+                    nid[k] = recs[jc].id;
+                }
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    const int32_t j = nj[k];
+                    const double s = ns[k];
                     if (j < 0 || !(s < INFINITY)) {
                         full = false;
                         continue;
                     }
                     sK = s > sK ? s : sK;
-                    if (pcomp[j] == mcomp) continue;  // also the point itself (INCL lists)
+                    if (ncomp[k] == mcomp) continue;  // also the point itself (INCL lists)
                     double mrd = sqrt(s);             // HDBSCANStar.java:162-168 order, as the scan kernel
                     if (mcore > mrd) mrd = mcore;
-                    const double oc = recs[j].core;
+                    const double oc = ncore[k];
                     if (oc > mrd) mrd = oc;
-                    const int32_t oid = recs[j].id;
+                    const int32_t oid = nid[k];
                     const int32_t lo = mid < oid ? mid : oid, hi = mid < oid ? oid : mid;
                     if (key_less(mrd, s, lo, hi, b)) {
                         b = Best{mrd, s, lo, hi};
