@@ -66,7 +66,7 @@ struct hdb_ctx {
     int64_t knn_mfma_min_n = 2048;
     bool knn_mfma_two_pass = true;  // K1m two-pass kernel (fallback): upper-bound pass first (few exact re-checks)
     bool knn_mfma_single = true;    // K1m single pass: screen + candidate log, FP64 re-check of the log
-    bool knn_mfma_prune = true;     // K1m single pass: random-projection order + FP64-ball superblock pruning
+    bool knn_mfma_prune = true;     // K1m single pass: k-means order + FP64-ball superblock pruning
     bool nearest_grouped = true;   // K3g: median-split sample groups + box pruning for big unkeyed scans
     bool boruvka_seed = true;      // seed Boruvka rounds from the previous round's edges
     int leaf_seed_k = -1;          // exact leaf: k-NN list length at least this (-1: by dimension)

@@ -74,12 +74,28 @@ int hdb_ctx_synchronize(hdb_ctx *ctx);
  *                                  (default 8192) and d in {1,2,3,4,8,16} use K1t, the
  *                                  box-pruned traversal of the Morton/BVH index, instead of
  *                                  the all-pairs K1;
+ *   "knn_mfma"        (default 1): euclidean lists with 16 < d <= 256 and n >= "knn_mfma_min_n"
+ *                                  (default 2048) use K1m (bf16-split MFMA screen, FP64 re-check);
+ *                                  "knn_mfma_single" (1: one screen pass + candidate log; 0: the
+ *                                  two-pass kernel, "knn_mfma_two_pass"), "knn_mfma_prune" (1:
+ *                                  k-means order + FP64-ball superblock pruning);
+ *   "nearest_grouped" (default 1): K3g (median-split sample groups, box pruning) for large
+ *                                  euclidean nearest-sample scans;
  *   "prim_coop"       (default 1): single-launch cooperative Prim for 4096 < n <= 65536;
+ *                                  "prim_coop_plain" (1: launched as a plain kernel first --
+ *                                  cooperative launches serialise device-wide -- with a timed-out
+ *                                  co-residency wait falling back to the cooperative launch),
+ *                                  "prim_coop_slots" (exchange layout);
  *   "boruvka_seed"    (default 1): a Boruvka round starts from the previous round's still
  *                                  valid per-point edges;
  *   "boruvka_knn_seed"(default 1): hdb_exact_mst seeds every Boruvka round from the k-NN
  *                                  lists (lanes whose seed is provably exact skip the scan);
- *   "count_evals"     (default 0): K1t counts the pairs it evaluates (read "last_evals"). */
+ *                                  "leaf_seed_k" (list length, -1: by dimension),
+ *                                  "leaf_list_rounds" (default 2: rounds seeded from the lists);
+ *   "boruvka_wave_pts" (default 64; 16/32/64): points per scan wave; "boruvka_early_pts" /
+ *                                  "boruvka_early_rounds": another size for the first rounds;
+ *   "trav_pop_test"   (default 0): bit 0 Boruvka, bit 1 K1t re-test a popped node;
+ *   "count_evals"     (default 0): K1t/K2b count the pairs they evaluate (read "last_evals"). */
 int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value);
 /* Diagnostic counters: "last_evals" = pair evaluations of the last K1t call (count_evals on). */
 int hdb_ctx_get_stat(hdb_ctx *ctx, const char *name, int64_t *value);
