@@ -364,6 +364,9 @@ constexpr int NW = HDB_K1S_WAVES;
 #ifndef HDB_K1S_XCD
 #define HDB_K1S_XCD 1  // contiguous query-group ranges per XCD (A/B at C4: screen 51.8 -> 50.7 ms)
 #endif
+#ifndef HDB_K1F_COMPACT
+#define HDB_K1F_COMPACT 1  // re-check: compact the surviving log entries first (A/B at C4: 23.6 -> 16.3 ms)
+#endif
 #ifndef HDB_K1F_XCD
 #define HDB_K1F_XCD 0  // the same for the re-check's query blocks
 #endif
@@ -996,10 +999,35 @@ __global__ __launch_bounds__(256) void knn_mfma_final_kernel(const double *__res
     double top[KC];
 #pragma unroll
     for (int k = 0; k < KC; k++) top[k] = INFINITY;
+#if HDB_K1F_COMPACT
+    // the entries that survive the final threshold are compacted first (ballot + prefix into
+    // LDS), so every lane streams a candidate row in each pass instead of idling on the
+    // entries lb > thr filters out; the KC smallest over the wave do not depend on which lane
+    // evaluated which candidate
+    __shared__ int cl_s[4][S_LOGCAP];
+    int *cl = cl_s[threadIdx.x >> 6];
+    int np = 0;
+    for (int j0 = 0; j0 < cnt; j0 += 64) {
+        const int j = j0 + lane;
+        bool ok = false;
+        int cid = 0;
+        if (j < cnt) {
+            const LogEnt e = logs[q * S_LOGCAP + j];
+            ok = e.lb <= t;
+            cid = e.cid;
+        }
+        const unsigned long long m = __ballot(ok);
+        if (ok) cl[np + __popcll(m & ((1ull << lane) - 1))] = cid;
+        np += __popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int j = lane; j < np; j += 64) topk_insert<KC>(top, exact_sq_pf(qr, X + (int64_t)perm[cl[j]] * d, d));
+#else
     for (int j = lane; j < cnt; j += 64) {
         const LogEnt e = logs[q * S_LOGCAP + j];
         if (e.lb <= t) topk_insert<KC>(top, exact_sq_pf(qr, X + (int64_t)perm[e.cid] * d, d));
     }
+#endif
     for (int k = 0; k < KC; k++) {
         double mn = top[0];
         for (int o = 32; o >= 1; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
