@@ -18,6 +18,7 @@ HDB_OK = 0
 ERRORS = {
     -1: "HDB_EINVAL", -2: "HDB_EDEVICE", -3: "HDB_ENOMEM", -10: "HDB_EREF_NPE", -11: "HDB_EREF_OOB",
     -12: "HDB_EREF_NEGATIVE_CLUSTER", -13: "HDB_EREF_DIVZERO", -14: "HDB_EREF_NUMBER_FORMAT",
+    -20: "HDB_EUNSUPPORTED",
 }
 
 METRIC = {"euclidean": 0, "cosine": 1, "pearson": 2, "manhattan": 3, "supremum": 4}

@@ -398,6 +398,7 @@ int hdb_local_model(hdb_ctx *ctx, const double *rep, const double *info, int64_t
         ctx->stats["lm_fosc_label_us"] += g_lm_us[4];
         ctx->stats["lm_fosc_noise_us"] += g_lm_us[5];
         ctx->stats["lm_calls"] += 1;
+        if (rc == HDB_EREF_NEGATIVE_CLUSTER) HDB_THROW(rc, local_model_error_detail());
         if (rc) HDB_THROW(rc, "local model raised a reference exception");
         std::copy(lab.begin(), lab.end(), labels);
         if (mst_va) std::copy(mva.begin(), mva.end(), mst_va);

@@ -180,23 +180,27 @@ int hdb_merge_edges(hdb_comm *comm, const int32_t *va, const int32_t *vb, const 
         const int64_t *ds = sg.in(seq, (size_t)e_local);
         const int R = comm->nranks;
         KernelTimer t(ctx, "merge_edges");
-        // 1. counts (and whether every rank passes seq: all or none)
+        // 1. counts (and whether every rank passes seq: all or none; a rank with no local
+        //    edges is consistent with either -- its seq pointer may well be NULL)
         int64_t *cnt_dev = nullptr;
         HIP_CHECK(hipMallocAsync((void **)&cnt_dev, sizeof(int64_t) * 2 * (R + 1), st));
-        int64_t mine[2] = {e_local, seq ? 1 : 0};
+        int64_t mine[2] = {e_local, e_local == 0 ? -1 : (seq ? 1 : 0)};
         HIP_CHECK(hipMemcpyAsync(cnt_dev + 2 * R, mine, sizeof(mine), hipMemcpyHostToDevice, st));
         RCCL_CHECK(rccl().all_gather(cnt_dev + 2 * R, cnt_dev, 2, ncclInt64, comm->comm, st));
         std::vector<int64_t> cnt(2 * R);
         HIP_CHECK(hipMemcpyAsync(cnt.data(), cnt_dev, sizeof(int64_t) * 2 * R, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
         std::vector<int64_t> offs(R + 1, 0);
-        int64_t maxc = 0, nseq = 0;
+        int64_t maxc = 0, with_seq = 0, without_seq = 0;
         for (int r = 0; r < R; r++) {
             offs[r + 1] = offs[r] + cnt[2 * r];
             maxc = std::max(maxc, cnt[2 * r]);
-            nseq += cnt[2 * r + 1];
+            with_seq += cnt[2 * r + 1] == 1;
+            without_seq += cnt[2 * r + 1] == 0;
         }
-        if (nseq != 0 && nseq != R) HDB_THROW(HDB_EINVAL, "merge_edges: seq must be given on every rank or on none");
+        if (with_seq && without_seq)
+            HDB_THROW(HDB_EINVAL, "merge_edges: seq must be given on every rank with local edges or on none");
+        const int64_t nseq = with_seq;
         const int64_t E = offs[R];
         // 2. padded blocks: [va | vb | w | seq] per rank
         const size_t blk = (size_t)maxc * (4 + 4 + 8 + (nseq ? 8 : 0));

@@ -78,6 +78,7 @@ struct hdb_ctx {
     int trav_pop_test = 0;         // bit 0: Boruvka re-tests a popped node, bit 1: K1t a popped leaf
     bool prim_coop = true;         // cooperative single-launch Prim for 4096 < n <= 65536
     bool prim_coop_plain = true;   // launch it as a plain kernel first (cooperative launches serialise)
+    int prim_coop_plain_spin_log2 = 20;  // plain attempt: polls per exchange before it reports non-co-residency
     int prim_coop_slots = 4;  // cooperative Prim exchange, rows in registers (d <= 16): 1 release/acquire slots, 2 granules,
                               // 3 drained sc1 slots, 4 DPP folds + key granules (default), 5 key+row granule sweep
     bool count_evals = false;  // K1t counts evaluated pairs (diagnostic; costs one sync)

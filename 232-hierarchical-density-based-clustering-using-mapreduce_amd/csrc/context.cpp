@@ -160,6 +160,7 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         hipDeviceProp_t prop;
         HIP_CHECK(hipGetDeviceProperties(&prop, device));
         c->num_cus = prop.multiProcessorCount;
+        c->stats["prim_coop_plain_retries"] = 0;
         if (const char *e = getenv("HDB_PRIM_COOP_SLOTS")) c->prim_coop_slots = atoi(e);  // A/B knob
         *out = c;
         return HDB_OK;
@@ -277,6 +278,11 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
     }
     if (k == "prim_coop_plain") {
         ctx->prim_coop_plain = value != 0;
+        return HDB_OK;
+    }
+    if (k == "prim_coop_plain_spin_log2") {
+        if (value < 0 || value > 24) return HDB_EINVAL;
+        ctx->prim_coop_plain_spin_log2 = (int)value;
         return HDB_OK;
     }
     if (k == "prim_coop") {

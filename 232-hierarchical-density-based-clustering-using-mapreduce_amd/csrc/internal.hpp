@@ -64,6 +64,8 @@ int bubble_core_epilogue(const double *rep, const int32_t *nB, const double *eB,
 int flat_labels_host(const int32_t *va, const int32_t *vb, const double *w, int64_t ne, int64_t n, int32_t mcs,
                      int32_t *labels, int64_t *n_clusters);
 int quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne);
+// message of the last HDB_EREF_NEGATIVE_CLUSTER on this thread (cluster label, level, numPoints)
+const char *local_model_error_detail();
 // host phase times of local_model_host (us): quicksort, cluster tree, FOSC + noise
 extern thread_local int64_t g_lm_us[6];  // + FOSC parts: selection walk, labelling, noise
 int local_model_host(const double *rep, const double *eB, const double *nnB, const int32_t *nB, int64_t b, int d,

@@ -8,6 +8,7 @@
 //   * findProminentClustersAndClassificationNoiseBubbles (:377-504),
 //   * findInterClusterEdges (:506-527).
 // Host C++ built with -ffp-contract=off so the few host distance evaluations match Java.
+#include <cstdio>
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -192,17 +193,55 @@ struct Dendro {
     }
 };
 
+thread_local char g_lm_detail[160];  // the reference's exception message + where it arose
+
+const char *local_model_error_detail() { return g_lm_detail; }
+
 static int detach(Cl &c, int32_t numPoints, double level) {  // Clusters.java:39-47
     c.numPoints -= numPoints;
     c.stability += ((double)(numPoints + 0) * (1 / level - 1 / c.birth));
     if (c.numPoints == 0) c.death = level;
-    else if (c.numPoints < 0) return HDB_EREF_NEGATIVE_CLUSTER;
+    else if (c.numPoints < 0) {
+        snprintf(g_lm_detail, sizeof(g_lm_detail),
+                 "Cluster cannot have less than 0 points. (label %d, level %.17g, numPoints %d)", (int)c.label, level,
+                 (int)c.numPoints);
+        return HDB_EREF_NEGATIVE_CLUSTER;
+    }
     return HDB_OK;
 }
 
 static uint32_t jhash(int32_t k) {
     uint32_t h = (uint32_t)k;
     return h ^ (h >> 16);
+}
+
+// Final capacity of a java.util.HashMap<Integer, ...> after putting `labels` (insertion
+// order) into a fresh map: 16 at the first put, doubled when size > 0.75 cap, and doubled
+// when a 9th key lands in one bucket of a table below 64 buckets (treeifyBin resizes
+// instead).  At >= 64 buckets such a bin becomes a tree bin, whose iteration order is not
+// emulated: -1 (HDB_EUNSUPPORTED).  Resizes split buckets order-preservingly, so the keySet
+// order is (bucket at the final capacity, insertion order).
+template <class Label>
+static int64_t jmap_capacity(const std::vector<Label> &aff) {
+    int64_t cap = 16;
+    std::vector<int32_t> cnt(cap, 0);
+    auto recount = [&](size_t upto) {
+        cnt.assign(cap, 0);
+        for (size_t j = 0; j <= upto; j++) cnt[jhash(aff[j].label) & (uint32_t)(cap - 1)]++;
+    };
+    for (size_t i = 0; i < aff.size(); i++) {
+        const int32_t before = cnt[jhash(aff[i].label) & (uint32_t)(cap - 1)]++;
+        if (before >= 8) {
+            if (cap >= 64) return -1;
+            cap *= 2;
+            recount(i);
+        }
+        if ((int64_t)(i + 1) > cap * 3 / 4) {
+            cap *= 2;
+            recount(i);
+        }
+    }
+    return cap;
 }
 
 
@@ -219,7 +258,7 @@ static int construct_cluster_tree_fast(int64_t b, const int32_t *ea, const int32
                                        int32_t mcl, const int32_t *nB, std::vector<Cl> &clusters, Dendro &D) {
     for (int64_t i = 0; i < ne; i++) {
         if (ea[i] < 0 || ea[i] >= b || eb[i] < 0 || eb[i] >= b) return HDB_EREF_OOB;
-        if (ew[i] != ew[i]) return HDB_EINVAL;  // NaN level: the reference's walk never advances
+        if (ew[i] != ew[i]) return HDB_EUNSUPPORTED;  // NaN level: the reference's walk never advances
     }
     // ---- bottom-up: pre-run component node of every edge endpoint
     D.b = b;
@@ -349,8 +388,8 @@ static int construct_cluster_tree_fast(int64_t b, const int32_t *ea, const int32
             }
         }
         if (aff.empty()) continue;
-        int64_t cap = 16;
-        while ((int64_t)aff.size() > cap * 3 / 4) cap *= 2;
+        const int64_t cap = jmap_capacity(aff);
+        if (cap < 0) return HDB_EUNSUPPORTED;
         std::stable_sort(aff.begin(), aff.end(), [&](const Aff &x, const Aff &y) {
             uint32_t bx = jhash(x.label) & (uint32_t)(cap - 1), by = jhash(y.label) & (uint32_t)(cap - 1);
             if (bx != by) return bx < by;
@@ -464,8 +503,8 @@ static int construct_cluster_tree_bfs(int64_t b, const int32_t *ea, const int32_
         }
         if (aff.empty()) continue;
         // java.util.HashMap key iteration: bucket order, insertion order inside a bucket
-        int64_t cap = 16;
-        while ((int64_t)aff.size() > cap * 3 / 4) cap *= 2;
+        const int64_t cap = jmap_capacity(aff);
+        if (cap < 0) return HDB_EUNSUPPORTED;
         std::stable_sort(aff.begin(), aff.end(), [&](const Aff &x, const Aff &y) {
             uint32_t bx = jhash(x.label) & (uint32_t)(cap - 1), by = jhash(y.label) & (uint32_t)(cap - 1);
             if (bx != by) return bx < by;

@@ -886,7 +886,8 @@ static bool launch_coop3(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
 template <int BS, int DM, bool FULL>
 __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int self_edges, int32_t *__restrict__ va,
                                                         int32_t *__restrict__ vb, double *__restrict__ w,
-                                                        gu64 *__restrict__ gkey, gu64 *__restrict__ grow, int *err) {
+                                                        gu64 *__restrict__ gkey, gu64 *__restrict__ grow, int *err,
+                                                        unsigned spin_limit) {
     constexpr int NW = BS / 64;
     constexpr int ND = DM + 3;  // x, core, eB, nnB
     __shared__ double s_cand[NW][ND + 1];
@@ -986,7 +987,7 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
                     s_key[j] = (unsigned)x;
                 }
                 if (__all(ok)) break;
-                if (++spins > (1u << 24)) {  // a co-residency failure must not hang the device
+                if (++spins > spin_limit) {  // a co-residency failure must not hang the device
                     if (lane == 0) atomicExch(err, 1);
                     tmo = true;
                     break;
@@ -1011,17 +1012,29 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
             } else {
                 if (FULL) {  // the winner's row is already in LDS
                     if (lane < 2 * ND) ((unsigned *)s_row)[lane] = s_key[KS * k + 3 + lane];
-                } else if (lane < 2 * ND) {  // the winner's row granules, straight into the LDS row
+                }
+                bool row_tmo = false;
+                if (!FULL && lane < 2 * ND) {  // the winner's row granules, straight into the LDS row
                     const gu64 *rb = grow + ((size_t)buf * nwg + k) * (2 * ND) + lane;
                     unsigned long long x;
                     for (unsigned spins = 0;;) {
                         x = __hip_atomic_load(rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if ((unsigned)(x >> 32) == tag || ++spins > (1u << 24)) break;
+                        if ((unsigned)(x >> 32) == tag) break;
+                        if (++spins > spin_limit) {  // a stale row must not be used: report, exit
+                            row_tmo = true;
+                            break;
+                        }
                         __builtin_amdgcn_s_sleep(1);
                     }
                     ((unsigned *)s_row)[lane] = (unsigned)x;
                 }
-                if (lane == 0) s_cur = win;
+                if (__any(row_tmo)) {
+                    if (lane == 0) {
+                        atomicExch(err, 1);
+                        s_cur = -1;
+                    }
+                } else if (lane == 0)
+                    s_cur = win;
             }
             COOP_T(4);
         }
@@ -1078,12 +1091,17 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
     int nn = (int)n;
     int32_t *pva = va + eo, *pvb = vb + eo;
     double *pw = w + eo;
-    void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &gkey, &grow, &err};
+    unsigned spin = 1u << 24;
+    void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &gkey, &grow, &err, &spin};
     // A plain launch first: ROCm serialises cooperative launches device-wide, so the concurrent
     // local models of one level (driver model pool) would queue behind each other.  The grid
     // (<= 64 workgroups) is far below the device's capacity, and every inter-workgroup wait has
     // a timeout: if the workgroups were not co-resident the kernel reports it and exits, the
-    // state is reset and the cooperative launch (guaranteed co-residency) runs instead.
+    // state is reset and the cooperative launch (guaranteed co-residency) runs instead.  The
+    // plain attempt waits at most 2^prim_coop_plain_spin_log2 polls per exchange (a step takes
+    // microseconds once every workgroup runs; the default 2^20 polls is ~1 s), the cooperative
+    // one 2^24.
+    const unsigned plain_spin = 1u << ctx->prim_coop_plain_spin_log2;
     int h_err = 0;
     for (int attempt = ctx->prim_coop_plain ? 0 : 1; attempt < 2; attempt++) {
         if (attempt == 1 && h_err) HIP_CHECK(hipMemsetAsync(base, 0, kbytes + rbytes + 256, ctx->stream));
@@ -1091,7 +1109,7 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
             KernelTimer t(ctx, "prim_coop");
             if (attempt == 0)
                 hipLaunchKernelGGL((prim_coop4_kernel<BS, DM, FULL>), dim3(nwg), dim3(BS), 0, ctx->stream, L, nn,
-                                   self_edges, pva, pvb, pw, gkey, grow, err);
+                                   self_edges, pva, pvb, pw, gkey, grow, err, plain_spin);
             else
                 HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_coop4_kernel<BS, DM, FULL>, dim3(nwg), dim3(BS),
                                                      args, 0, ctx->stream));

@@ -121,7 +121,9 @@ def _merge_via_comm(comm: HdbComm, va, vb, w, seq):
     ctx = comm.ctx
     pa, pb, pw = C.c_void_p(), C.c_void_p(), C.c_void_p()
     e = C.c_int64()
-    s = seq.contiguous() if seq is not None else None
+    # an empty tensor's data_ptr() is 0: the library treats a rank with no local edges as
+    # consistent with either seq mode, so NULL is fine there
+    s = seq.to(torch.int64).contiguous() if seq is not None else None
     A.check(A.lib().hdb_merge_edges(comm.h, va.data_ptr(), vb.data_ptr(), w.data_ptr(),
                                     s.data_ptr() if s is not None else None, w.shape[0], C.byref(pa), C.byref(pb),
                                     C.byref(pw), C.byref(e)), "hdb_merge_edges")

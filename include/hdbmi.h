@@ -36,6 +36,9 @@ extern "C" {
 #define HDB_EREF_NEGATIVE_CLUSTER (-12) /* Clusters.java:45-46 "Cluster cannot have less than 0 points." */
 #define HDB_EREF_DIVZERO (-13)          /* java.lang.ArithmeticException: / by zero          */
 #define HDB_EREF_NUMBER_FORMAT (-14)    /* java.lang.NumberFormatException                   */
+#define HDB_EUNSUPPORTED (-20)          /* a reference behaviour not emulated: a treeified
+                                           java.util.HashMap bin (iteration order) or a loop the
+                                           reference never leaves (NaN edge weight)            */
 
 /* DistanceCalculator.getName() (distance/DistanceCalculator.java:20) */
 #define HDB_METRIC_EUCLIDEAN 0 /* EuclideanDistance.java:28-36  */
@@ -84,7 +87,10 @@ int hdb_ctx_synchronize(hdb_ctx *ctx);
  *   "prim_coop"       (default 1): single-launch cooperative Prim for 4096 < n <= 65536;
  *                                  "prim_coop_plain" (1: launched as a plain kernel first --
  *                                  cooperative launches serialise device-wide -- with a timed-out
- *                                  co-residency wait falling back to the cooperative launch),
+ *                                  co-residency wait falling back to the cooperative launch;
+ *                                  stat "prim_coop_plain_retries" counts those fallbacks),
+ *                                  "prim_coop_plain_spin_log2" (default 20: polls per exchange
+ *                                  before the plain attempt reports non-co-residency),
  *                                  "prim_coop_slots" (exchange layout);
  *   "boruvka_seed"    (default 1): a Boruvka round starts from the previous round's still
  *                                  valid per-point edges;
@@ -218,7 +224,8 @@ int hdb_copy(hdb_ctx *ctx, void *dst, const void *src, int64_t bytes);
 /* Main.java:302-347 + UnionFindReducer.call + SortMST (UnionFindReducer.java:19-69,
  * SortMST.java:9-17): every rank passes its local edge list; all ranks receive the merged
  * list of all E edges (device memory allocated by the library, freed with hdb_free), stably
- * sorted by DESCENDING weight.  seq (nullable; on every rank or on none): the canonical
+ * sorted by DESCENDING weight.  seq (nullable; on every rank that has local edges or on
+ * none -- a rank with e_local == 0 is consistent with either): the canonical
  * position of each local edge in the global concatenation (a permutation of [0, E) over all
  * ranks) -- the sort then sees that concatenation, independent of which rank computed which
  * partition; NULL = rank-major concatenation.  Collective; synchronises. */

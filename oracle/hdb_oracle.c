@@ -32,6 +32,9 @@
 #define ORC_EREF_OOB (-11)              /* ArrayIndexOutOfBoundsException            */
 #define ORC_EREF_NEGATIVE_CLUSTER (-12) /* Clusters.java:45-46 IllegalStateException */
 #define ORC_EREF_DIVZERO (-13)          /* java.lang.ArithmeticException (int / 0)   */
+#define ORC_EUNSUPPORTED (-20)          /* a Java behaviour not emulated: a treeified HashMap bin
+                                           (its iteration order changes) or a loop the reference
+                                           never leaves (NaN edge weight in the cluster tree) */
 
 enum { M_EUCLIDEAN = 0, M_COSINE = 1, M_PEARSON = 2, M_MANHATTAN = 3, M_SUPREMUM = 4 };
 enum { CORE_INCL_SELF_CUMULATIVE = 0, CORE_INCL_SELF = 1, CORE_EXCL_SELF = 2 };
@@ -587,22 +590,64 @@ static int cl_push(clvec *x, cl_t c) {
     x->c[x->n++] = c;
     return 0;
 }
+/* the state at the last "Cluster cannot have less than 0 points." (test diagnostics) */
+static __thread int32_t g_neg_label, g_neg_points;
+static __thread double g_neg_level;
+int orc_last_negative_cluster(int32_t *label, double *level, int32_t *num_points) {
+    *label = g_neg_label;
+    *level = g_neg_level;
+    *num_points = g_neg_points;
+    return ORC_OK;
+}
 static int cl_detach(cl_t *c, int32_t numPoints, int32_t countMembers, double level) {
     c->numPoints -= numPoints;
     c->stability += ((double)(numPoints + countMembers) * (1 / level - 1 / c->birth));
     if (c->numPoints == 0) c->death = level;
-    else if (c->numPoints < 0) return ORC_EREF_NEGATIVE_CLUSTER;
+    else if (c->numPoints < 0) {
+        g_neg_label = c->label;
+        g_neg_level = level;
+        g_neg_points = c->numPoints;
+        return ORC_EREF_NEGATIVE_CLUSTER;
+    }
     return ORC_OK;
 }
 
 /* ---- java.util.HashMap<Integer, ...> key iteration order emulation:
  * bucket = spread(h) & (cap-1) with spread(h) = h ^ (h >>> 16); buckets ascending,
- * insertion order within a bucket; cap = 16 doubling while size > 0.75*cap.
- * (Tree bins, >= 8 keys in one bucket at cap >= 64, are not emulated.) */
+ * insertion order within a bucket (resizes split buckets order-preservingly).  The final
+ * capacity replays the puts: 16 at the first put, doubled when size > 0.75*cap, and doubled
+ * when a 9th key lands in one bucket of a table smaller than 64 (treeifyBin resizes instead);
+ * at >= 64 buckets that bin becomes a tree bin, whose iteration order is not emulated:
+ * ORC_EUNSUPPORTED. */
 static uint32_t jhash(int32_t k) { uint32_t h = (uint32_t)k; return h ^ (h >> 16); }
-static int64_t jmap_cap(int64_t size) {
+static int64_t jmap_cap(const int32_t *keys, int64_t n) { /* keys in insertion order */
     int64_t cap = 16;
-    while (size > (cap * 3) / 4) cap *= 2;
+    int64_t *cnt = (int64_t *)calloc((size_t)cap, sizeof(int64_t));
+    if (!cnt) return -1;
+    for (int64_t i = 0; i < n; i++) {
+        for (int pass = 0; pass < 2; pass++) {
+            const int64_t before = cnt[jhash(keys[i]) & (uint32_t)(cap - 1)];
+            int grow = 0;
+            if (pass == 0) {
+                cnt[jhash(keys[i]) & (uint32_t)(cap - 1)]++;
+                if (before >= 8) {
+                    if (cap >= 64) { free(cnt); return -2; }
+                    grow = 1;
+                }
+            } else if (i + 1 > (cap * 3) / 4) {
+                grow = 1;
+            }
+            if (grow) {
+                cap *= 2;
+                int64_t *nc = (int64_t *)calloc((size_t)cap, sizeof(int64_t));
+                if (!nc) { free(cnt); return -1; }
+                for (int64_t j = 0; j <= i; j++) nc[jhash(keys[j]) & (uint32_t)(cap - 1)]++;
+                free(cnt);
+                cnt = nc;
+            }
+        }
+    }
+    free(cnt);
     return cap;
 }
 
@@ -680,6 +725,7 @@ static int construct_cluster_tree(int64_t b, const int32_t *ea, const int32_t *e
         aff_t *aff = NULL;
         int64_t naff = 0, affcap = 0;
         double cw = ew[cur];
+        if (cw != cw) { rc = ORC_EUNSUPPORTED; goto out; } /* the Java loop never advances */
         while (cur >= 0 && ew[cur] == cw) {
             int32_t f = ea[cur], s = eb[cur];
             iv_remove_first(&adj[f], s);
@@ -700,7 +746,19 @@ static int construct_cluster_tree(int64_t b, const int32_t *ea, const int32_t *e
             cur--;
         }
         if (naff == 0) { free(aff); continue; }
-        g_cap_for_sort = jmap_cap(naff);
+        {
+            int32_t *keys = (int32_t *)malloc(sizeof(int32_t) * (size_t)naff);
+            if (!keys) { free(aff); rc = ORC_ENOMEM; goto out; }
+            for (int64_t k = 0; k < naff; k++) keys[k] = aff[k].label;
+            g_cap_for_sort = jmap_cap(keys, naff);
+            free(keys);
+            if (g_cap_for_sort < 0) {
+                for (int64_t k = 0; k < naff; k++) free(aff[k].verts);
+                free(aff);
+                rc = g_cap_for_sort == -2 ? ORC_EUNSUPPORTED : ORC_ENOMEM;
+                goto out;
+            }
+        }
         qsort(aff, (size_t)naff, sizeof(aff_t), cmp_aff);
 
         for (int64_t ai = 0; ai < naff && rc == ORC_OK; ai++) {

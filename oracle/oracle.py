@@ -23,7 +23,7 @@ INCL_SELF_CUMULATIVE, INCL_SELF, EXCL_SELF = range(3)
 JMAX = np.finfo(np.float64).max
 
 ERRORS = {-1: "EINVAL", -3: "ENOMEM", -10: "EREF_NPE", -11: "EREF_OOB",
-          -12: "EREF_NEGATIVE_CLUSTER", -13: "EREF_DIVZERO"}
+          -12: "EREF_NEGATIVE_CLUSTER", -13: "EREF_DIVZERO", -20: "EUNSUPPORTED"}
 
 
 class OracleError(RuntimeError):
@@ -294,6 +294,14 @@ def local_model(rep, info, min_pts, min_cl_size, metric="euclidean"):
                                nic.ctypes.data_as(C.POINTER(C.c_int64))), "local_model")
     k = int(nic[0])
     return dict(labels=labels, mst=(mva, mvb, mw), inter=(iva[:k], ivb[:k], iw[:k]))
+
+
+def last_negative_cluster():
+    """(label, level, numPoints) of the cluster whose detachPoints threw last on this thread
+    (Clusters.java:45-46) -- test diagnostics."""
+    lab, lev, pts = C.c_int32(), C.c_double(), C.c_int32()
+    lib().orc_last_negative_cluster(C.byref(lab), C.byref(lev), C.byref(pts))
+    return dict(label=lab.value, level=lev.value, num_points=pts.value)
 
 
 def first_step_leaf(X, ids, min_pts, metric="euclidean"):

@@ -80,3 +80,17 @@ def test_c1_full_skin_boruvka_leaf(pkg, skin):
     assert np.array_equal(w, G["w"])  # merged list is sorted descending: multiset equality
     assert got["n_clusters"] == int(G["n_clusters"])
     assert np.array_equal(got["labels"].cpu().numpy(), G["labels"])
+
+
+def test_c1_level0_model_raises_where_the_transcriptions_do(pkg):
+    """C1's level-0 model (18,135 Skin bubbles; tests/golden/make_c1_level0.py): the product's
+    local model raises the reference's exception at the cluster label, level and point count
+    where both independent transcriptions (pure Python, C oracle) throw."""
+    z = golden("c1_level0_model")
+    with pytest.raises(pkg.IllegalStateException) as ei:
+        pkg.LocalModelReduceByKey(int(z["min_pts"]), int(z["mcl"])).call(z["rep"], z["info"])
+    import re
+    m = re.search(r"\(label (-?\d+), level ([^,]+), numPoints (-?\d+)\)", str(ei.value))
+    assert m, str(ei.value)
+    assert (int(m.group(1)), float(m.group(2)), int(m.group(3))) == \
+        (int(z["label"]), float(z["level"]), int(z["num_points"]))

@@ -455,6 +455,28 @@ def test_prim_cooperative_vs_oracle(pkg, oracle, n, kind):
         assert eq(g.getVerticeA(), va) and eq(g.getVericeB(), vb) and eq(g.getEges(), w), (coop, slots)
 
 
+def test_prim_coop_plain_timeout_retries_cooperatively(pkg, oracle):
+    """A plain-launched cooperative Prim whose inter-workgroup waits time out (forced here with a
+    2-poll limit) must report it -- key sweep and winner-row wait alike -- and the cooperative
+    relaunch must give the reference Prim exactly (prim.hip row-wait timeout)."""
+    X = blobs(12000, 3, 7, 77)
+    core = oracle.core_distances(X, 4, semantics=0)
+    va, vb, w = oracle.prim_mst(X, core)
+    ctx = pkg.Context.get(0)
+    star = pkg.HDBSCANStar(ctx)
+    before = ctx.get_stat("prim_coop_plain_retries")
+    for slots in (4, 5):
+        ctx.set_option("prim_coop_slots", slots)
+        ctx.set_option("prim_coop_plain_spin_log2", 0)
+        try:
+            g = star.constructMST(X, core, True)
+        finally:
+            ctx.set_option("prim_coop_plain_spin_log2", 20)
+            ctx.set_option("prim_coop_slots", 4)
+        assert eq(g.getVerticeA(), va) and eq(g.getVericeB(), vb) and eq(g.getEges(), w), slots
+    assert ctx.get_stat("prim_coop_plain_retries") >= before + 1
+
+
 @pytest.mark.parametrize("d,metric,n", [(8, "euclidean", 9000), (16, "euclidean", 5000), (5, "cosine", 6000),
                                         (2, "manhattan", 4500)])
 def test_prim_coop_slots_metrics_and_bubbles(pkg, oracle, d, metric, n):

@@ -112,6 +112,9 @@ def _comm_worker(rank, world, port, out_dir):
     except pkg.HdbError:
         bad = True
     assert bad, "a non-permutation seq must be rejected"
+    # a rank with no local edges passes an empty seq (data_ptr() == 0): accepted
+    e0 = P.merge_local_msts(t(va[:0]), t(vb[:0]), t(w[:0]), seq=t(seq[:0]), comm=comm)
+    assert all(x.shape[0] == 0 for x in e0)
     comm.close()
     dist.destroy_process_group()
 
