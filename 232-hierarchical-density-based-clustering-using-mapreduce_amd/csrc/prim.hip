@@ -1118,7 +1118,11 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
         h_err = 0;
         HIP_CHECK(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
         HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        if (!h_err) return true;
+        if (!h_err) {
+            ctx->stats["prim_coop_steps"] += n - 1;  // sequential Prim steps (roofline: bench.py)
+            ctx->stats["prim_coop_launches"] += 1;
+            return true;
+        }
         if (attempt == 0) ctx->stats["prim_coop_plain_retries"] += 1;
     }
     HDB_THROW(HDB_EDEVICE, "prim_coop: key sweep timed out (workgroups not co-resident)");

@@ -61,6 +61,17 @@ def cpu_model():
     return "unknown"
 
 
+def host_threads():
+    """CPU threads this process may run on (the affinity mask, not the machine's CPU count),
+    capped by OMP_NUM_THREADS when set."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(aff, omp) if omp > 0 else aff
+
+
 def cpu_baseline(X, budget_s=10.0):
     """Oracle (line-faithful C restatement, -O2) on a bounded sample of the same workload:
     k-NN core distances for R query rows against all n rows (n^2 work per point,
@@ -72,7 +83,7 @@ def cpu_baseline(X, budget_s=10.0):
     from oracle import oracle as O
     O.lib()
     n = X.shape[0]
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = host_threads()
 
     def sample(T, budget):
         core_rows = (lambda Xs, r: O.core_rows(Xs, r, MIN_PTS)) if T == 1 else \
@@ -105,7 +116,7 @@ def cpu_baseline(X, budget_s=10.0):
     tot_all, r_all, m_all = sample(threads, budget_s)
     tot_1, r_1, m_1 = sample(1, budget_s)
     return {"value": n / tot_all, "unit": "points/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
             "sample": f"oracle C -O2, OpenMP {threads} threads: kNN of {r_all} query rows vs all {n} rows "
                       f"(x{n / r_all:.0f}) + reference Prim (parallel scan per step) on a {m_all}-point prefix "
                       f"(x{(n / m_all) ** 2:.0f}); extrapolated full step {tot_all:.0f} s",
@@ -194,6 +205,8 @@ def run_c4(args):
                        "points": n, "d": d, "min_pts": mp,
                        "timed": "pinned host X -> H2D -> K1m core distances -> D2H of the cores"},
             "mrd_evals_per_s": n * (n - 1) / dt,
+            "mrd_evals_per_s_kind": "algorithmic-equivalent: n(n-1) pairs of the k-NN over the step time",
+            "executed_pair_evals_per_s": pairs / dt,
             "roofline": {"bound": "mfma", "kernel": "knn_mfma_screen_kernel (K1m)", "achieved": issued / k_s / 1e12,
                          "peak": MFMA_BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                          "frac": issued / k_s / 1e12 / MFMA_BF16_DENSE_TFLOPS,
@@ -208,7 +221,7 @@ def run_c4(args):
     if not args.no_cpu_baseline:
         from oracle import oracle as O
         O.lib()
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        threads = host_threads()
         Xh = X_pin.numpy()
         rows = np.linspace(0, n - 1, 16 * threads).astype(np.int64)
         t0 = time.perf_counter()
@@ -232,6 +245,63 @@ PARTITIONED = {  # SURVEY.md §8(d) C3 / C5 (recursive sampling, data bubbles), 
 }
 
 
+TIMED_KERNELS = ("prim_coop", "prim_block", "prim_step_total", "knn_tree", "boruvka_scan", "boruvka_total",
+                 "leaf_core", "knn_generic", "nearest_grouped", "nearest_sq", "nearest_generic", "bubble_knn",
+                 "bubble_stats", "merge_sort", "merge_edges", "flat_labels")
+# K2b's launches sit inside boruvka_total; exact_leaf_total / boruvka_total nest other timers
+NESTED = {"boruvka_scan"}
+
+
+def partitioned_roofline(kt, coop_steps, coop_launches, steps):
+    """Latency roofline of the cooperative Prim (prim_coop: the bubble models' and the big
+    leaves' reference Prim, the level loop's critical path): every Prim step needs at least
+    one inter-workgroup exchange through the device-coherent cache -- the winner's key
+    published by a store and observed by a load of every workgroup, two dependent
+    Infinity-Cache round trips (MI355X_MICROARCH.md: 227 ns each).  Lower bound = steps x
+    2 x 227 ns; frac = bound / measured prim_coop time."""
+    t = kt.get("prim_coop", [0.0, 0])[0] / steps
+    s = coop_steps / steps
+    bound = s * 2 * MALL_HIT_NS * 1e-9
+    top = max(((k, v[0]) for k, v in kt.items() if k not in NESTED), key=lambda x: x[1], default=(None, 0.0))
+    return {"bound": "latency", "kernel": "prim_coop4_kernel (cooperative reference Prim, HdbscanDataBubbles.java:"
+                                          "165-254 / HDBSCANStar.java:124-205)",
+            "unit": "Prim steps/s", "achieved": s / t if t > 0 else 0.0,
+            "peak": 1.0 / (2 * MALL_HIT_NS * 1e-9), "frac": bound / t if t > 0 else 0.0, "traffic": None,
+            "model": "per step: 2 dependent Infinity-Cache round trips (publish the workgroup minimum, observe "
+                     f"every workgroup's) x {MALL_HIT_NS:.0f} ns",
+            "steps_per_job": s, "launches_per_job": coop_launches / steps, "kernel_s_per_job": t,
+            "us_per_step": t / s * 1e6 if s else None,
+            "dominant_kernel": top[0], "dominant_kernel_s": top[1] / steps}
+
+
+CPU_SAMPLES = {  # the partitioned configs' family at a size the serial oracle runs in ~10-30 s
+    "c3": dict(n=50_000, d=16, centers=50, spread=50.0, seed=3, samples_per_subset=512, processing_units=4096),
+    "c5": dict(n=50_000, d=8, centers=100, spread=100.0, seed=5, samples_per_subset=1024, processing_units=4096),
+}
+
+
+def partitioned_cpu_baseline(workload):
+    """The oracle's MR-HDBSCAN* loop (oracle/mr_driver.py over hdb_oracle.c, -O2, one thread:
+    the reference runs one Spark task per subset and setMaster("local") is one thread,
+    Main.java:89) on a 50k-point instance of the config's family, samples per subset and
+    processing_units scaled down with it; flat labels left out (the reference never computes
+    them).  points/s of that instance -- the loop is superlinear in n, so the full-size CPU
+    rate would be lower still."""
+    from oracle import mr_driver as M
+    cs = CPU_SAMPLES[workload]
+    rng = np.random.default_rng(cs["seed"])
+    C = rng.uniform(-cs["spread"], cs["spread"], size=(cs["centers"], cs["d"]))
+    X = C[rng.integers(0, cs["centers"], size=cs["n"])] + rng.normal(0, 1.0, size=(cs["n"], cs["d"]))
+    t0 = time.perf_counter()
+    r = M.run(X, min_pts=MIN_PTS, min_cl_size=MIN_CL_SIZE, processing_units=cs["processing_units"],
+              samples_per_subset=cs["samples_per_subset"], flat=False)
+    dt = time.perf_counter() - t0
+    return {"value": cs["n"] / dt, "unit": "points/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"oracle MR-HDBSCAN* loop (mr_driver, C -O2, 1 thread) on {cs['n']} x {cs['d']} blobs "
+                      f"({cs['centers']} centres, seed {cs['seed']}), samples/subset {cs['samples_per_subset']}, "
+                      f"processing_units {cs['processing_units']}: {r['iterations']} levels in {dt:.1f} s"}
+
+
 def run_partitioned(args, workload):
     """C3 / C5: the whole MR-HDBSCAN* job (every level, the merge, the flat labels) on N GPUs
     with the sharded driver; every rank holds the parsed points (pinned host memory), the
@@ -239,6 +309,7 @@ def run_partitioned(args, workload):
     scaling: the same job at every N; value = points / job time."""
     import torch
     import torch.distributed as dist
+    os.environ.setdefault("HDB_KERNEL_TIMING", "1")  # every context (model threads too) times its kernels
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -254,7 +325,7 @@ def run_partitioned(args, workload):
     X_pin = torch.from_numpy(C[rng.integers(0, cfg["centers"], size=n)] +
                              rng.normal(0, 1.0, size=(n, cfg["d"]))).pin_memory()
     drv = pkg.MRHDBSCANStar(minPts=MIN_PTS, minClSize=MIN_CL_SIZE, processing_units=cfg["processing_units"],
-                            samples_per_subset=cfg["samples_per_subset"], prim_leaf_max=4096, profile=args.phases)
+                            samples_per_subset=cfg["samples_per_subset"], profile=args.phases)
     out = {}
 
     if os.environ.get("HDB_WATCHDOG"):  # diagnosis: every thread's Python stack every N s
@@ -275,9 +346,29 @@ def run_partitioned(args, workload):
             dist.barrier()
         torch.cuda.synchronize()
 
+    def kernel_totals(reset=True):
+        """summed device time (s) and launches per timed kernel over every context (driver
+        thread + model threads), HIP events on each context's stream"""
+        tot = {}
+        for c in list(A.Context._all):
+            for k in TIMED_KERNELS:
+                ms, calls = c.kernel_time(k, reset)
+                if calls:
+                    a = tot.setdefault(k, [0.0, 0])
+                    a[0] += ms / 1e3
+                    a[1] += calls
+        return tot
+
+    def stat_total(name, reset_to=None):
+        return sum(c.get_stat(name) for c in list(A.Context._all))
+
     for _ in range(args.warmup):
         job()
     barrier()
+    kernel_totals()
+    steps0 = stat_total("prim_coop_steps")
+    launches0 = stat_total("prim_coop_launches")
+    retries0 = stat_total("prim_coop_plain_retries")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         job()
@@ -287,6 +378,10 @@ def run_partitioned(args, workload):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     r = out["r"]
+    kt = kernel_totals()
+    coop_steps = stat_total("prim_coop_steps") - steps0
+    coop_launches = stat_total("prim_coop_launches") - launches0
+    coop_retries = stat_total("prim_coop_plain_retries") - retries0
     if rank == 0:
         w = out["edges"][2].numpy()
         assert w.shape[0] == 2 * n - 1 and np.all(w[:-1] >= w[1:])
@@ -297,7 +392,7 @@ def run_partitioned(args, workload):
                 "scaling": "strong", "vs_baseline": None, "dtype": "f64",
                 "data": f"synthetic (seeded Gaussian blobs, seed {cfg['seed']})",
                 "config": {"workload": cfg["desc"], "points": n, "d": cfg["d"], "min_pts": MIN_PTS,
-                           "min_cl_size": MIN_CL_SIZE, "prim_leaf_max": 4096,
+                           "min_cl_size": MIN_CL_SIZE, "prim_leaf_max": drv.prim_leaf_max,
                            "parallelism": f"sharded driver x{world} (leaves/local models by LPT, "
                                           f"point-chunked nearest sample, RCCL merge)"},
                 "iterations": r["iterations"], "n_clusters": r["n_clusters"],
@@ -308,7 +403,12 @@ def run_partitioned(args, workload):
                                    ("core", "prim", "quicksort", "tree", "fosc", "fosc_select", "fosc_label",
                                     "fosc_noise")} |
                                   {"calls": A.Context.stat_total("lm_calls")}) if args.phases else None,
-                "roofline": None}
+                "kernels_s": {k: round(v[0] / args.steps, 4) for k, v in sorted(kt.items(), key=lambda x: -x[1][0])},
+                "kernel_launches": {k: v[1] // args.steps for k, v in kt.items()},
+                "prim_coop_plain_retries": coop_retries,
+                "roofline": partitioned_roofline(kt, coop_steps, coop_launches, args.steps)}
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = partitioned_cpu_baseline(workload)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -508,6 +608,10 @@ def main():
         "device_resident_points_per_s": total_points * tsteps / dt_dev,
         "device_resident_ms_per_step": dt_dev * 1e3 / tsteps,
         "mrd_evals_per_s": evals * tsteps / dt,
+        "mrd_evals_per_s_kind": "algorithmic-equivalent: n^2 (k-NN) + n(n-1)/2 (MST) per partition (SURVEY.md "
+                                "8(d)) over the step time; the exact pruned kernels execute ~1/1000 of it "
+                                "(executed_pair_evals_per_s)",
+        "executed_pair_evals_per_s": world * (knn_evals + bor_evals) * tsteps / dt,
         "kernels_ms_per_step": ms,
         "executed_pair_evals_per_step": {"knn_tree": knn_evals, "boruvka_scan": bor_evals,
                                          "algorithmic": n * n + n * (n - 1) // 2},

@@ -42,7 +42,7 @@ def sample_ids(n_key: int, k: float, samples_per_subset: int | None, seed: int, 
 
 
 def run(X, min_pts=4, min_cl_size=4, processing_units=50, k=0.2, samples_per_subset=None, seed=20210101,
-        metric="euclidean", all_inter_edges=True, max_levels=64, log=None):
+        metric="euclidean", all_inter_edges=True, max_levels=64, log=None, flat=True):
     """Returns dict(edges=(va, vb, w) merged (stable, descending weight), levels=[...],
     leaf_of=np.array subset key of the leaf that processed each point, iterations)."""
     X = np.ascontiguousarray(X, np.float64)
@@ -137,7 +137,7 @@ def run(X, min_pts=4, min_cl_size=4, processing_units=50, k=0.2, samples_per_sub
         levels.append(level)
     va, vb, w = O.merge_edges(edge_lists)                  # UnionFindReducer + SortMST
     out = dict(edges=(va, vb, w), levels=levels, leaf_of=leaf_of, iterations=iteration)
-    if all_inter_edges:                                    # D6: global flat labels
+    if all_inter_edges and flat:                           # D6: global flat labels (O(levels n))
         from .flat_labels import flat_labels
         out["labels"], out["n_clusters"] = flat_labels(n, va, vb, w, min_cl_size)
     return out

@@ -16,7 +16,8 @@ def run_both(pkg, X, **kw):
     got = pkg.MRHDBSCANStar(minPts=kw.get("min_pts", 4), minClSize=kw.get("min_cl_size", 4),
                             processing_units=kw["processing_units"], k=kw.get("k", 0.2),
                             samples_per_subset=kw.get("samples_per_subset"),
-                            all_inter_edges=kw.get("all_inter_edges", True)).run(X)
+                            all_inter_edges=kw.get("all_inter_edges", True),
+                            distanceFunction=kw.get("metric")).run(X)
     return ref, got
 
 
@@ -56,6 +57,17 @@ def test_driver_samples_per_subset(pkg):
     X = blobs(6000, 2, 8, 4)
     ref, got = run_both(pkg, X, processing_units=800, samples_per_subset=200)
     check(ref, got)
+
+
+@pytest.mark.parametrize("n,pu,k", [(6000, 6000, 0.2), (20000, 9000, 0.05)])
+def test_driver_cosine_forced_leaf_above_4096(pkg, n, pu, k):
+    """a non-Euclidean metric (CosineSimilarity.java:28-40) with d = 5 and leaves of
+    4,096-65,536 points: K2b does not apply (driver.py boruvka_ok), so those leaves run the
+    reference Prim (cooperative launch) -- the whole run must equal the oracle's loop."""
+    X = blobs(n, 5, 7, n, spread=20.0) + 25.0  # off the origin: cosine distances spread out
+    ref, got = run_both(pkg, X, processing_units=pu, k=k, metric="cosine")
+    check(ref, got)
+    assert max(max(L["leaves"].values(), default=0) for L in got["levels"]) > 4096
 
 
 def test_flat_labels_device_inputs(pkg, oracle):
