@@ -201,7 +201,7 @@ __global__ void build_recs_kernel(const double *__restrict__ X, const double *__
 constexpr int SG = 16;
 constexpr int NSG = BT / SG;
 #ifndef HDB_LEAF_PREFETCH
-#define HDB_LEAF_PREFETCH 1
+#define HDB_LEAF_PREFETCH 0  // measured 8.74 -> 8.67 ms with per-lane tests; with HDB_BOR_SUBTEST it spills
 #endif
 #ifndef HDB_K1T_PREFETCH  // the same prefetch in K1t: off -- 82 -> 104 VGPRs drops K1t to 4
 #define HDB_K1T_PREFETCH 0  // waves/SIMD and costs more than it hides (2.0 -> 2.23 ms)
@@ -542,6 +542,73 @@ __device__ __forceinline__ void push_children(const Bvh &bvh, const int64_t *off
     sp += __popc(okmask);
 }
 
+#ifndef HDB_BOR_SUBTEST
+#define HDB_BOR_SUBTEST 1  // K2b child / group tests lane-parallel against 8-lane subgroup boxes
+#endif
+// The same push with a lane-parallel pre-filter: lane L tests child L & 7 against the box of
+// its 8-lane subgroup L >> 3 (ok(a, b, tag): a superset of what the subgroup's lanes need),
+// then only the children that pass are tested per lane (needs) -- the same children as
+// push_children, with one wave-wide test plus one per surviving child instead of one per child.
+template <int D, class SubOk, class Needs>
+__device__ __forceinline__ void push_children_sub(const Bvh &bvh, const int64_t *off_s, const int64_t *cnt_s, int lev,
+                                                  int64_t idx, const double *qlo, const double *qhi, int32_t *stk,
+                                                  int &sp, int lane, double *sb, int32_t *st, SubOk ok, Needs needs) {
+    const int64_t c0 = idx * FAN;
+    const int64_t c1 = min(c0 + FAN, cnt_s[lev - 1]);
+    const int64_t base = off_s[lev - 1] + c0;
+    const int nc = (int)(c1 - c0);
+    stage_boxes<D, FAN>(bvh.lo + base * D, bvh.hi + base * D, bvh.tag + base, nc, sb, st, lane);
+    const int k = lane & (FAN - 1);
+    bool need = false;
+    if (k < nc) {
+        double a[D], b[D];
+#pragma unroll
+        for (int c = 0; c < D; c++) {
+            a[c] = sb[k * D + c];
+            b[c] = sb[FAN * D + k * D + c];
+        }
+        need = ok(a, b, st[k]);
+    }
+    unsigned long long m = __ballot(need);
+    m |= m >> 32;
+    m |= m >> 16;
+    m |= m >> 8;
+    const unsigned pre = __builtin_amdgcn_readfirstlane((unsigned)(m & 0xffu));
+    if (pre == 0) return;
+    unsigned okmask = 0;
+#pragma unroll 1
+    for (unsigned r = pre; r; r &= r - 1) {
+        const int kk = __builtin_ctz(r);
+        double a[D], b[D];
+        staged_box<D, FAN>(sb, kk, a, b);
+        if (__any(needs(a, b, st[kk]))) okmask |= 1u << kk;
+    }
+    okmask = __builtin_amdgcn_readfirstlane(okmask);
+    if (okmask == 0) return;
+    double key = -1.0;
+    const bool mine = lane < FAN && ((okmask >> lane) & 1u);
+    if (mine) {
+        double kk = 0;
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            const double g = fmax(fmax(sb[lane * D + d] - qhi[d], qlo[d] - sb[FAN * D + lane * D + d]), 0.0);
+            kk = kk + g * g;
+        }
+        key = kk;
+    }
+    int rank = 0;
+#pragma unroll
+    for (int j = 0; j < FAN; j++) {
+        const double kj = __shfl(key, j);
+        const bool okj = (okmask >> j) & 1u;
+        rank += (okj && (kj > key || (kj == key && j < lane))) ? 1 : 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (mine) stk[sp + rank] = ((lev - 1) << 26) | (int32_t)(c0 + lane);
+    __builtin_amdgcn_wave_barrier();
+    sp += __popc(okmask);
+}
+
 // Publishes min(v) per component into arr with few atomics: late rounds put most of the
 // n lanes into a handful of components, and one atomicMin per lane on the same address
 // serialises in L2.  A wave whose active lanes share one component reduces first; any
@@ -584,6 +651,9 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
     __shared__ int32_t boxt_s[4][FAN];
     __shared__ int64_t lvl_s[4][2 * (MAXLEV + 1)];
     __shared__ double q_s[4][2 * D];
+#if HDB_BOR_SUBTEST
+    __shared__ double sg_s[4][8 * 2 * D];
+#endif
     const int w = threadIdx.x >> 6;
     double *bxs = boxs_s[w];
     int32_t *bxt = boxt_s[w];
@@ -669,6 +739,75 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
         }
     }
     __builtin_amdgcn_wave_barrier();
+#if HDB_BOR_SUBTEST
+    // 8-lane subgroups (consecutive work entries: Morton-close points).  Every node and group
+    // test below runs once per (child, subgroup) pair on its own lane, with the box of the
+    // subgroup's points, the largest bound among its searching lanes and the component they
+    // all share (-2: mixed or none).  Exact: the box-to-box gap (monotone rounding) is <= the
+    // gap of every point of the subgroup, so a child no subgroup needs is needed by no lane.
+    // subgroup boxes parked in LDS (registers would spill): [8][lo D | hi D]
+    double *sgb = sg_s[w];
+#pragma unroll
+    for (int c = 0; c < D; c++) {
+        const bool nan = !(mx[c] == mx[c]);  // a NaN coordinate needs every box (its gaps are 0)
+        double l = valid ? (nan ? -INFINITY : mx[c]) : INFINITY, h = valid ? (nan ? INFINITY : mx[c]) : -INFINITY;
+#pragma unroll
+        for (int off = 1; off < 8; off <<= 1) {
+            l = fmin(l, __shfl_xor(l, off));
+            h = fmax(h, __shfl_xor(h, off));
+        }
+        if ((lane & 7) == 0) {
+            sgb[(lane >> 3) * 2 * D + c] = l;
+            sgb[(lane >> 3) * 2 * D + D + c] = h;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const double *sgl = sgb + (lane >> 3) * 2 * D, *sgh = sgl + D;
+    int32_t ucomp;
+    {
+        int32_t cmn = search ? mcomp : INT32_MAX, cmx = search ? mcomp : INT32_MIN;
+#pragma unroll
+        for (int off = 1; off < 8; off <<= 1) {
+            cmn = min(cmn, __shfl_xor(cmn, off));
+            cmx = max(cmx, __shfl_xor(cmx, off));
+        }
+        ucomp = cmn == cmx ? cmn : -2;
+    }
+    // the subgroup's largest bound over its lanes still searching (-1: none)
+    auto sub_bound = [&]() -> double {
+        double m = (search & !(mlb > cwv)) ? bound() : -1.0;
+#pragma unroll
+        for (int off = 1; off < 8; off <<= 1) m = fmax(m, __shfl_xor(m, off));
+        return m;
+    };
+    auto sub_ok = [&](double mb) {
+        return [&, mb](const double (&a)[D], const double (&b)[D], int32_t tg) -> bool {
+            double lb = 0;
+#pragma unroll
+            for (int c = 0; c < D; c++) {
+                const double g = fmax(fmax(a[c] - sgh[c], sgl[c] - b[c]), 0.0);
+                lb = lb + g * g;
+            }
+            return (mb >= 0.0) & !((tg >= 0) & (tg == ucomp)) & !(lb > mb);
+        };
+    };
+    // needed 16-point groups of the staged leaf: lane L tests group L & 7 (< NSG)
+    auto group_mask = [&]() -> unsigned {
+        const double mb = sub_bound();
+        const int k = lane & 7;
+        bool need = false;
+        if (k < NSG) {
+            double a[D], bb[D];
+            staged_box<D, NSG>(bxs, k, a, bb);
+            need = sub_ok(mb)(a, bb, bxt[k]);
+        }
+        unsigned long long m = __ballot(need);
+        m |= m >> 32;
+        m |= m >> 16;
+        m |= m >> 8;
+        return __builtin_amdgcn_readfirstlane((unsigned)(m & ((1u << NSG) - 1)));
+    };
+#endif
     level_table(ntiles, off_s, cnt_s, lane);
     int sp = 0;
     if (lane == 0) stk[0] = ((bvh.levels - 1) << 26) | 0;
@@ -694,7 +833,12 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
             if (!__any(needs_vals(a, bb, bxt[0]))) continue;
         }
         if (lev > 0) {
+#if HDB_BOR_SUBTEST
+            push_children_sub<D>(bvh, off_s, cnt_s, lev, idx, qlo, qhi, stk, sp, lane, bxs, bxt, sub_ok(sub_bound()),
+                                 needs_vals);
+#else
             push_children<D>(bvh, off_s, cnt_s, lev, idx, qlo, qhi, stk, sp, lane, bxs, bxt, needs_vals);
+#endif
             continue;
         }
         // leaf: tile idx, 4 groups of 16 candidates.  The tile's records are fetched with one
@@ -733,10 +877,14 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
             staged_box<D, NSG>(bxs, gi, a, bb);
             return needs_vals(a, bb, bxt[gi]);
         };
+#if HDB_BOR_SUBTEST
+        const unsigned gmask = group_mask();  // pre-filter; the per-lane test below decides
+#else
         unsigned gmask = 0;
 #pragma unroll 1
         for (int gi = 0; gi < NSG; gi++)
             if (__any(gneeds(gi))) gmask |= 1u << gi;
+#endif
         if (gmask == 0) continue;
 #pragma unroll 1
         for (int gi = 0; gi < NSG; gi++) {
