@@ -329,6 +329,154 @@ __global__ void dc_link(DC c, int b, int j, int64_t nl) {
     }
 }
 
+// Deep depths in one launch, in parallel: a workgroup takes a block of 2^LB consecutive ranks
+// whose labels name the components of F_{<lo} and runs the same rank divide and conquer on
+// LDS (labels hashed to local ids, contracted labels = HS + local root-edge rank, an LDS
+// union-find with the global kernels' randomised linking, LDS atomics for the component
+// root edge / size / smallest id).  Every edge whose local bits are not all ones is a
+// component root edge at exactly one local depth (trailing ones) and gets |C(e)| and min id
+// there; the block's last edge got them at a global depth.  Parents inside the block are set
+// here, the others were set by the global depths.
+template <int LB>
+struct DcBlk {
+    static constexpr int B = 1 << LB, HS = 4 * B, NL = HS + B;
+};
+
+__device__ __forceinline__ int32_t lds_find(int32_t *uf, int32_t x) {
+    while (true) {
+        const int32_t p = ((volatile int32_t *)uf)[x];
+        if (p == x) return x;
+        const int32_t g = ((volatile int32_t *)uf)[p];
+        if (g == p) return p;
+        ((volatile int32_t *)uf)[x] = g;
+        x = g;
+    }
+}
+
+template <int LB, int TB>
+__global__ __launch_bounds__(TB) void dc_block(DC c, int *__restrict__ err) {
+    using P = DcBlk<LB>;
+    __shared__ int32_t key[P::HS], bsz[P::HS], bmn[P::HS];             // hashed labels, base size / min id
+    __shared__ int32_t uf[P::NL], re[P::NL], cs[P::NL], cm[P::NL];     // per label (per depth)
+    __shared__ int8_t stp[P::NL];                                      // local depth stamp
+    __shared__ int16_t lab[2 * P::B];                                  // endpoint labels (local ids)
+    __shared__ int32_t esz[P::B], emn[P::B], lpar[P::B];
+    __shared__ int16_t hk[P::B], rp[P::B];
+    __shared__ int s_err;
+    const int t = threadIdx.x;
+    for (int64_t lo = (int64_t)blockIdx.x * P::B; lo < c.m; lo += (int64_t)gridDim.x * P::B) {
+        const int cnt = (int)(c.m - lo < P::B ? c.m - lo : P::B);
+        for (int k = t; k < P::HS; k += TB) key[k] = -1;
+        for (int k = t; k < P::NL; k += TB) stp[k] = -1;
+        for (int k = t; k < P::B; k += TB) {
+            esz[k] = -1;
+            lpar[k] = INT32_MAX;
+        }
+        if (t == 0) s_err = 0;
+        __syncthreads();
+        for (int k = t; k < 2 * cnt; k += TB) {
+            const int32_t x = c.lab[2 * lo + k];
+            uint32_t h = uf_prio(x, 0) & (P::HS - 1);
+            while (true) {  // <= 2B keys in 4B slots
+                const int32_t old = atomicCAS(&key[h], -1, x);
+                if (old == -1) {
+                    bsz[h] = x < c.n ? 1 : c.esize[x - c.n];
+                    bmn[h] = x < c.n ? x : c.eminid[x - c.n];
+                    break;
+                }
+                if (old == x) break;
+                h = (h + 1) & (P::HS - 1);
+            }
+            lab[k] = (int16_t)h;
+        }
+        __syncthreads();
+        for (int b = LB - 1; b >= 0; b--) {
+            const int half = 1 << b, nl = (P::B >> 1);
+            // L edges: local ranks with bit b clear
+            for (int i = t; i < nl; i += TB) {
+                const int k = ((i >> b) << (b + 1)) | (i & (half - 1));
+                if (k >= cnt) continue;
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    const int x = lab[2 * k + s];
+                    uf[x] = x;
+                    re[x] = -1;
+                    cs[x] = x < P::HS ? bsz[x] : esz[x - P::HS];
+                    cm[x] = x < P::HS ? bmn[x] : emn[x - P::HS];
+                    stp[x] = (int8_t)b;
+                }
+            }
+            __syncthreads();
+            for (int i = t; i < nl; i += TB) {
+                const int k = ((i >> b) << (b + 1)) | (i & (half - 1));
+                if (k >= cnt) continue;
+                int32_t a = lab[2 * k], d = lab[2 * k + 1], hooked = -1;
+                while (true) {
+                    a = lds_find(uf, a);
+                    d = lds_find(uf, d);
+                    if (a == d) break;
+                    const uint32_t pa = uf_prio(a, P::HS), pd = uf_prio(d, P::HS);
+                    if (pa < pd || (pa == pd && a < d)) {
+                        const int32_t tt = a;
+                        a = d;
+                        d = tt;
+                    }
+                    if (atomicCAS(&uf[d], d, a) == d) {
+                        hooked = d;
+                        break;
+                    }
+                }
+                if (hooked < 0) s_err = 1;
+                hk[k] = (int16_t)hooked;
+            }
+            __syncthreads();
+            for (int i = t; i < nl; i += TB) {
+                const int k = ((i >> b) << (b + 1)) | (i & (half - 1));
+                if (k >= cnt) continue;
+                const int32_t rep = lds_find(uf, lab[2 * k]);
+                rp[k] = (int16_t)rep;
+                atomicMax(&re[rep], k);
+                const int32_t x = hk[k];
+                if (x >= 0) {  // a hooked label is never a representative: its cs / cm are its base
+                    atomicAdd(&cs[rep], cs[x]);
+                    atomicMin(&cm[rep], cm[x]);
+                }
+            }
+            __syncthreads();
+            for (int i = t; i < nl; i += TB) {
+                const int k = ((i >> b) << (b + 1)) | (i & (half - 1));
+                if (k >= cnt) continue;
+                const int32_t rep = rp[k];
+                if (re[rep] == k) {
+                    esz[k] = cs[rep];
+                    emn[k] = cm[rep];
+                }
+                const int u = k | half;
+                if (u >= cnt) continue;
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    const int x = lab[2 * u + s];
+                    if (stp[x] == (int8_t)b) {
+                        const int32_t R = re[lds_find(uf, x)];
+                        atomicMin(&lpar[R], u);
+                        lab[2 * u + s] = (int16_t)(P::HS + R);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        for (int k = t; k < cnt; k += TB) {
+            if (esz[k] >= 0) {
+                c.esize[lo + k] = esz[k];
+                c.eminid[lo + k] = emn[k];
+            }
+            if (lpar[k] != INT32_MAX) c.parent[lo + k] = (int32_t)(lo + lpar[k]);
+        }
+        if (t == 0 && s_err) atomicOr(err, FE_CYCLE);
+        __syncthreads();
+    }
+}
+
 // Deep depths in one launch: a block of LOC_EDGES consecutive ranks whose labels name the
 // components of F_{<lo} runs the sequential Kruskal process itself (one wave per block, the
 // block's labels hashed to LDS slots, union by size, one lane walking the ranks in order):
@@ -417,10 +565,16 @@ __global__ void fl_jump(int32_t *__restrict__ up, int64_t m, const int *__restri
     int ch = 0;
     HDB_GRID_STRIDE(r, m) {
         int32_t p = up[r];
-        int32_t g = up[p];
-        if (g != p) {
-            int32_t h = up[g];  // two hops per round
-            up[r] = h;
+        bool moved = false;
+#pragma unroll 1
+        for (int it = 0; it < 2; it++) {  // two hops per step, two steps per launch
+            const int32_t g = up[p];
+            if (g == p) break;
+            p = up[g];
+            moved = true;
+        }
+        if (moved) {
+            up[r] = p;
             ch = 1;
         }
     }
@@ -470,7 +624,8 @@ __global__ void fl_terms(const int32_t *__restrict__ top, const int32_t *__restr
                          const int32_t *__restrict__ cs, const int32_t *__restrict__ cid,
                          const int32_t *__restrict__ esize, const int32_t *__restrict__ nvalid,
                          const int32_t *__restrict__ vsum, const double *__restrict__ ew, int64_t m, int32_t mcs,
-                         uint64_t *__restrict__ key, double *__restrict__ val) {
+                         uint64_t *__restrict__ key, double *__restrict__ val, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
     HDB_GRID_STRIDE(r, m) {
         uint64_t k = ~uint64_t(0);
         double v = 0.0;
@@ -497,10 +652,12 @@ __global__ void fl_terms(const int32_t *__restrict__ top, const int32_t *__restr
 // in flight), lane 0 adds them in order -- the host's sequential sum, descending level
 constexpr int STAB_CHUNK = 256;
 __global__ __launch_bounds__(64) void fl_stab(const double *__restrict__ val, const int32_t *__restrict__ seg_lo,
-                                              const int32_t *__restrict__ seg_hi, int32_t nc,
-                                              double *__restrict__ stab) {
+                                              const int32_t *__restrict__ seg_hi, const int32_t *__restrict__ Kp,
+                                              double *__restrict__ stab, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
     __shared__ double buf[STAB_CHUNK];
     const int lane = threadIdx.x;
+    const int32_t nc = *Kp;
     for (int32_t c = blockIdx.x; c < nc; c += gridDim.x) {
         const int64_t lo = seg_lo[c], hi = lo < 0 ? -1 : seg_hi[c];
         double s = 0.0;
@@ -529,7 +686,8 @@ __global__ __launch_bounds__(64) void fl_stab(const double *__restrict__ val, co
 }
 
 __global__ void fl_seg(const uint64_t *__restrict__ key, int64_t m, int32_t *__restrict__ seg_lo,
-                       int32_t *__restrict__ seg_hi) {
+                       int32_t *__restrict__ seg_hi, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
     HDB_GRID_STRIDE(i, m) {
         uint64_t k = key[i];
         if (k == ~uint64_t(0)) continue;
@@ -541,24 +699,474 @@ __global__ void fl_seg(const uint64_t *__restrict__ key, int64_t m, int32_t *__r
 
 __global__ void fl_cluster_meta(const int32_t *__restrict__ is_start, const int32_t *__restrict__ cid,
                                 const int32_t *__restrict__ cs, const int32_t *__restrict__ pnode,
-                                const int32_t *__restrict__ eminid, int64_t m, int32_t *__restrict__ cpar,
-                                int32_t *__restrict__ cmin) {
+                                const int32_t *__restrict__ eminid, const int32_t *__restrict__ esize, int64_t m,
+                                int32_t *__restrict__ cpar, int32_t *__restrict__ cmin, int32_t *__restrict__ csz,
+                                int32_t *__restrict__ Kp, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
     HDB_GRID_STRIDE(r, m) {
+        if (r == m - 1) *Kp = cid[r] + 1;  // the root (rank m-1) always starts a cluster
         if (!is_start[r]) continue;
         int32_t c = cid[r];
         int32_t P = pnode[r];
         cpar[c] = P == NONE ? -1 : cid[cs[P]];
         cmin[c] = eminid[r];
+        csz[c] = esize[r];
     }
 }
 
+// ------------------------------------------------------ 5. FOSC over the cluster tree
+// (HDBSCANStar.java:567-625 propagateTree / findProminentClusters with flat.cpp step 3's
+// canonical rules).  Clusters 0..K-1, a child's id below its parent's, the root K-1.  The
+// bottom-up pass contrib(c) = stab(c) if stab(c) >= (sum of the children's contribs, summed
+// in ascending smallest point id) else that sum, must reproduce the host's floating-point
+// order exactly, so it is never re-associated: the tree is cut into heavy paths (heavy child
+// = most points, so a root-leaf path crosses <= log2(n) light edges) and ONE wave walks a
+// path bottom-up, the running value in a register, the light children's values already
+// final.  A path starts when its last light child path finishes (last-arriver continuation
+// inside one launch: no level-synchronous launches).  Selection = the topmost self-selected
+// cluster below the root on every chain (pointer jumping); labels 1..K by smallest point id.
+__device__ __forceinline__ uint64_t pk(int32_t lo, int32_t hi) { return (uint32_t)lo | ((uint64_t)(uint32_t)hi << 32); }
+__device__ __forceinline__ int32_t pk_lo(uint64_t w) { return (int32_t)(uint32_t)w; }
+__device__ __forceinline__ int32_t pk_hi(uint64_t w) { return (int32_t)(uint32_t)(w >> 32); }
+
+__global__ void fo_children(const int32_t *__restrict__ cpar, const int32_t *__restrict__ csz,
+                            const int32_t *__restrict__ Kp, int32_t *__restrict__ nch,
+                            unsigned long long *__restrict__ hkey, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    const int32_t K = *Kp;
+    HDB_GRID_STRIDE(c, K - 1) {
+        const int32_t p = cpar[c];
+        if ((uint32_t)p >= (uint32_t)K) continue;  // malformed input (reported by the caller)
+        atomicAdd(&nch[p], 1);
+        atomicMax(&hkey[p], (unsigned long long)pk((int32_t)c, csz[c]));  // (points, id): heavy child
+    }
+}
+
+__global__ void fo_kids_fill(const int32_t *__restrict__ cpar, const int32_t *__restrict__ Kp,
+                             const int32_t *__restrict__ kstart, int32_t *__restrict__ kcur, int32_t *__restrict__ kids, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    const int32_t K = *Kp;
+    HDB_GRID_STRIDE(c, K - 1) {
+        const int32_t p = cpar[c];
+        if ((uint32_t)p >= (uint32_t)K) continue;
+        const int32_t slot = kstart[p] + atomicAdd(&kcur[p], 1);
+        if (slot < K) kids[slot] = (int32_t)c;
+    }
+}
+
+// multi-way nodes: children in ascending smallest point id (disjoint clusters: distinct ids);
+// heavy-path word: (ancestor, distance) -- a heavy child points to its parent at distance 1
+__global__ void fo_paths_init(const int32_t *__restrict__ cpar, const int32_t *__restrict__ cmin,
+                              const int32_t *__restrict__ Kp, const int32_t *__restrict__ nch,
+                              const unsigned long long *__restrict__ hkey, const int32_t *__restrict__ kstart,
+                              int32_t *__restrict__ kids, uint64_t *__restrict__ jw, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    const int32_t K = *Kp;
+    HDB_GRID_STRIDE(c, K) {
+        const int32_t p = c == K - 1 ? -1 : cpar[c];
+        const bool heavy = p >= 0 && p < K && pk_lo(hkey[p]) == (int32_t)c;
+        jw[c] = heavy ? pk(p, 1) : pk((int32_t)c, 0);
+        const int32_t k = nch[c];
+        if (k > 2) {  // insertion sort by smallest id (few, small segments)
+            int32_t *s = kids + kstart[c];
+            for (int32_t i = 1; i < k; i++) {
+                const int32_t x = s[i], key = cmin[x];
+                int32_t j = i - 1;
+                while (j >= 0 && cmin[s[j]] > key) {
+                    s[j + 1] = s[j];
+                    j--;
+                }
+                s[j + 1] = x;
+            }
+        }
+    }
+}
+
+// pointer jumping over packed (ancestor, accumulated sum) words; a word whose ancestor is
+// itself is final.  Words are read and written whole, so a stale read is a valid shorter jump.
+__global__ void fo_jump_sum(uint64_t *__restrict__ jw, const int32_t *__restrict__ Kp, const int *__restrict__ flag_prev,
+                            int *__restrict__ flag_next, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    if (flag_prev && *flag_prev == 0) return;
+    const int32_t K = *Kp;
+    int ch = 0;
+    HDB_GRID_STRIDE(c, K) {
+        uint64_t w = jw[c];
+        bool moved = false;
+#pragma unroll 1
+        for (int it = 0; it < 3; it++) {  // several doublings per launch (fewer launches)
+            const int32_t a = pk_lo(w);
+            if (a == (int32_t)c) break;
+            const uint64_t w2 = jw[a];
+            const int32_t a2 = pk_lo(w2);
+            if (a2 == a) break;
+            w = pk(a2, pk_hi(w) + pk_hi(w2));
+            moved = true;
+        }
+        if (moved) {
+            jw[c] = w;
+            ch = 1;
+        }
+    }
+    flag_or(flag_next, ch);
+}
+
+// per path (top t): length (from its bottom leaf); light-depth word of a top = (top of the
+// parent's path, 1), jumped to (root path, number of light edges above it)
+__global__ void fo_paths_meta(const int32_t *__restrict__ cpar, const int32_t *__restrict__ Kp,
+                              const int32_t *__restrict__ nch, const uint64_t *__restrict__ jw,
+                              int32_t *__restrict__ plen, uint64_t *__restrict__ lw, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    const int32_t K = *Kp;
+    HDB_GRID_STRIDE(c, K) {
+        const uint64_t w = jw[c];
+        const int32_t top = pk_lo(w);
+        if (nch[c] == 0) plen[top] = pk_hi(w) + 1;  // every path ends at exactly one leaf
+        lw[c] = top == (int32_t)c && c != K - 1 ? pk(pk_lo(jw[cpar[c]]), 1) : pk((int32_t)c, 0);
+    }
+}
+
+// path node lists, by position from the top; the deepest light depth
+__global__ void fo_paths_nodes(const int32_t *__restrict__ Kp, const uint64_t *__restrict__ jw,
+                               const int32_t *__restrict__ poff, const uint64_t *__restrict__ lw,
+                               int32_t *__restrict__ nodes, int *__restrict__ maxld, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    const int32_t K = *Kp;
+    int32_t mx = 0;
+    HDB_GRID_STRIDE(c, K) {
+        const uint64_t w = jw[c];
+        const int32_t top = pk_lo(w);
+        const int64_t at = (int64_t)poff[top] + pk_hi(w);
+        if (at >= 0 && at < K) nodes[at] = (int32_t)c;
+        if (top == (int32_t)c) mx = max(mx, pk_hi(lw[c]));
+    }
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0 && mx > 0) atomicMax(maxld, mx);
+}
+
+// path-ordered node records (cluster, light child / -2 leaf / -1 multi-way, stability), the
+// multi-way node list, and a flag on paths holding a multi-way node wider than FO_WIDE
+constexpr int FO_CHUNK = 64, FO_SHORT = 48, FO_WIDE = 8;
+__global__ void fo_paths_rec(const int32_t *__restrict__ Kp, const int32_t *__restrict__ nodes,
+                             const int32_t *__restrict__ nch, const unsigned long long *__restrict__ hkey,
+                             const int32_t *__restrict__ kstart, const int32_t *__restrict__ kids,
+                             const double *__restrict__ stab, int32_t *__restrict__ rc, int32_t *__restrict__ rl,
+                             double *__restrict__ rs, int32_t *__restrict__ mlist, int32_t *__restrict__ mcount,
+                             const uint64_t *__restrict__ jw, int32_t *__restrict__ pwide, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    const int32_t K = *Kp;
+    auto top_of = [&](int32_t c) { return pk_lo(jw[c]); };
+    HDB_GRID_STRIDE(i, K) {
+        const int32_t c = nodes[i];
+        const int32_t k = nch[c];
+        int32_t lt = -2;
+        if (k == 2) {
+            const int32_t h = pk_lo(hkey[c]), k0 = kids[kstart[c]], k1 = kids[kstart[c] + 1];
+            lt = k0 == h ? k1 : k0;
+        } else if (k > 0) {
+            lt = -1;
+            mlist[atomicAdd(mcount, 1)] = c;
+            if (k > FO_WIDE) atomicOr(&pwide[top_of(c)], 1);  // its path runs wave-cooperatively
+        }
+        rc[i] = c;
+        rl[i] = lt;
+        rs[i] = stab[c];
+    }
+}
+
+// paths walked by a whole wave (long, or holding a wide multi-way node), one list for all levels
+__global__ void fo_long_list(const int32_t *__restrict__ Kp, const uint64_t *__restrict__ jw,
+                             const int32_t *__restrict__ plen, const int32_t *__restrict__ pwide,
+                             int32_t *__restrict__ llist, int32_t *__restrict__ lcount, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    const int32_t K = *Kp;
+    HDB_GRID_STRIDE(c, K) {
+        if (pk_lo(jw[c]) == (int32_t)c && (plen[c] > FO_SHORT || pwide[c])) llist[atomicAdd(lcount, 1)] = (int32_t)c;
+    }
+}
+
+struct FoscArr {
+    const int32_t *cpar, *nch, *kstart, *kids, *plen, *poff, *rc, *rl, *Kp, *mlist, *mcount, *pwide, *llist, *lcount;
+    const double *rs;
+    const uint64_t *jw, *lw;
+    const unsigned long long *hkey;
+    const int *maxld;
+    int32_t *ssel, *hpos;      // hpos: the heavy child's place among a multi-way node's children
+    double *cp, *pre, *postv;  // pre: per multi-way node; postv: aligned with kids
+};
+
+__device__ __forceinline__ double readlane_d(double x, int l) {  // l: wave-uniform
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ int32_t fo_level(const FoscArr &a, int32_t c) { return pk_hi(a.lw[pk_lo(a.jw[c])]); }
+
+// multi-way nodes on the paths of light depth d: their light children are final.  The sum
+// before the heavy child (from 0.0, ascending smallest id) is formed here; the values after
+// it are staged for the walker, which adds them after the heavy child's value.
+__global__ __launch_bounds__(64) void fo_multi_pre(FoscArr a, int d, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    if (d > *a.maxld) return;
+    __shared__ double sv[64];
+    const int lane = threadIdx.x;
+    const int32_t M = *a.mcount;
+    for (int32_t j = blockIdx.x; j < M; j += gridDim.x) {
+        const int32_t c = a.mlist[j];
+        if (fo_level(a, c) != d) continue;
+        const int32_t k = a.nch[c], k0 = a.kstart[c], h = pk_lo(a.hkey[c]);
+        double s = 0.0;
+        int32_t hpos = -1;  // the heavy child's position once seen
+        for (int32_t q0 = 0; q0 < k; q0 += 64) {
+            const int32_t q = q0 + lane;
+            const int32_t x = q < k ? a.kids[k0 + q] : -1;
+            const double v = (q < k && x != h) ? a.cp[x] : 0.0;
+            const uint64_t hb = __ballot(x == h);
+            const int lim = hpos >= 0 ? 0 : (hb ? __ffsll((unsigned long long)hb) - 1 : min(64, k - q0));
+            if (hb) hpos = q0 + __ffsll((unsigned long long)hb) - 1;
+            if (hpos >= 0 && q > hpos && q < k) a.postv[k0 + q] = v;  // added after the heavy child
+            sv[lane] = v;
+            __syncthreads();
+            if (lane == 0)
+                for (int i = 0; i < lim; i++) s = s + sv[i];  // before it, from 0.0
+            __syncthreads();
+        }
+        if (lane == 0) {
+            a.pre[c] = s;
+            a.hpos[c] = hpos;
+        }
+    }
+}
+
+// one node of the chain: the host's additions and comparison, in its order
+__device__ __forceinline__ double fo_node(const FoscArr &a, int32_t c, int32_t lt, double st, double lv, double acc,
+                                          int32_t &self) {
+    double prop;
+    if (lt == -2) {
+        self = 1;
+        return st;
+    }
+    if (lt >= 0) {
+        prop = acc + lv;  // binary: a + b == b + a
+    } else {              // multi-way: (sum before the heavy child) + heavy, then the ones after it
+        prop = a.pre[c] + acc;
+        const int32_t k = a.nch[c], k0 = a.kstart[c];
+        for (int32_t q = a.hpos[c] + 1; q < k; q++) prop = prop + a.postv[k0 + q];
+    }
+    self = st >= prop;  // Cluster.propagate: ties keep the parent
+    return self ? st : prop;
+}
+
+// paths of light depth d (launched deepest first: a path's light children are final when it
+// runs).  Long paths (and paths holding a wide multi-way node) from the list: one wave each,
+// 64 records at a time staged in LDS, lane 0 running the chain, the whole wave staging a
+// multi-way node's values after its heavy child.  Short paths: one lane each, walking its
+// records bottom-up with the next record's loads in flight.
+__global__ __launch_bounds__(64) void fo_walk(FoscArr a, int d, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    if (d > *a.maxld) return;
+    __shared__ double s_st[FO_CHUNK], s_lv[FO_CHUNK], s_out[FO_CHUNK];
+    __shared__ int32_t s_sel[FO_CHUNK];
+    const int lane = threadIdx.x;
+    const int32_t K = *a.Kp, NL = *a.lcount;
+    for (int32_t j = blockIdx.x; j < NL; j += gridDim.x) {
+        const int32_t t = a.llist[j];
+        if (pk_hi(a.lw[t]) != d) continue;
+        const int32_t tlen = min(a.plen[t], K), toff = a.poff[t], tstop = t == K - 1 ? 1 : 0;
+        double acc = 0.0;  // the running value, the same in every lane
+        for (int32_t hi = tlen - 1; hi >= tstop; hi -= FO_CHUNK) {
+            const int cnt = min(FO_CHUNK, hi - tstop + 1);
+            int32_t c = 0, lt = -2;
+            if (lane < cnt) {  // step q of the chunk = the record q above its bottom
+                const int32_t i = toff + hi - lane;
+                c = a.rc[i];
+                lt = a.rl[i];
+                s_st[lane] = a.rs[i];
+                s_lv[lane] = lt >= 0 ? a.cp[lt] : 0.0;
+            }
+            const uint64_t multi = __ballot(lane < cnt && lt == -1);
+            __syncthreads();
+            int i = 0;
+            if (hi == tlen - 1) {  // the path's bottom: a leaf, its own stability
+                acc = s_st[0];
+                s_out[0] = acc;
+                s_sel[0] = 1;
+                i = 1;
+            }
+            while (i < cnt) {
+                const uint64_t mr = i < 64 ? multi & (~0ull << i) : 0;
+                const int e = mr ? min(cnt, __ffsll((unsigned long long)mr) - 1) : cnt;
+                int q = i;
+                for (; q + 8 <= e; q += 8) {  // binary nodes: uniform LDS reads ahead of the chain
+                    double st8[8], lv8[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        st8[u] = s_st[q + u];
+                        lv8[u] = s_lv[q + u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const double prop = acc + lv8[u];  // binary: a + b == b + a
+                        const bool sq = st8[u] >= prop;    // ties keep the parent
+                        acc = sq ? st8[u] : prop;
+                        s_out[q + u] = acc;
+                        s_sel[q + u] = sq;
+                    }
+                }
+                for (; q < e; q++) {
+                    const double st1 = s_st[q], prop = acc + s_lv[q];
+                    const bool sq = st1 >= prop;
+                    acc = sq ? st1 : prop;
+                    s_out[q] = acc;
+                    s_sel[q] = sq;
+                }
+                if (e < cnt) {  // a multi-way node: (sum before the heavy child) + heavy + the rest
+                    const int32_t cm = __builtin_amdgcn_readlane(c, e);
+                    const double stm = s_st[e];
+                    const int32_t k = a.nch[cm], k0 = a.kstart[cm];
+                    double prop = a.pre[cm] + acc;
+                    for (int32_t q0 = a.hpos[cm] + 1; q0 < k; q0 += 64) {
+                        const int32_t qq = q0 + lane;
+                        const double pv = qq < k ? a.postv[k0 + qq] : 0.0;
+                        const int lim = min(64, k - q0);
+                        for (int r = 0; r < lim; r++) prop = prop + readlane_d(pv, r);
+                    }
+                    const bool sm = stm >= prop;
+                    acc = sm ? stm : prop;
+                    s_out[e] = acc;
+                    s_sel[e] = sm;
+                    i = e + 1;
+                } else {
+                    i = e;
+                }
+            }
+            __syncthreads();
+            if (lane < cnt) {
+                a.cp[c] = s_out[lane];
+                a.ssel[c] = s_sel[lane];
+            }
+            __syncthreads();
+        }
+    }
+    for (int32_t base = blockIdx.x * 64; base < K; base += gridDim.x * 64) {
+        const int32_t me = base + lane;
+        if (me >= K || pk_lo(a.jw[me]) != me || pk_hi(a.lw[me]) != d) continue;
+        const int32_t len = min(a.plen[me], K), off = a.poff[me];
+        if (len > FO_SHORT || a.pwide[me]) continue;  // a wave's path
+        const int32_t stop = me == K - 1 ? 1 : 0;  // the root's own contribution is never used
+        double acc = 0.0;
+        int32_t hi = len - 1;
+        int32_t c = 0, lt = -2;
+        double st = 0.0, lv = 0.0;
+        if (hi >= stop) {
+            c = a.rc[off + hi];
+            lt = a.rl[off + hi];
+            st = a.rs[off + hi];
+            lv = lt >= 0 ? a.cp[lt] : 0.0;
+        }
+        for (; hi >= stop; hi--) {
+            int32_t c2 = 0, lt2 = -2;
+            double st2 = 0.0, lv2 = 0.0;
+            if (hi - 1 >= stop) {  // next record in flight while this one is evaluated
+                c2 = a.rc[off + hi - 1];
+                lt2 = a.rl[off + hi - 1];
+                st2 = a.rs[off + hi - 1];
+                lv2 = lt2 >= 0 ? a.cp[lt2] : 0.0;
+            }
+            int32_t self;
+            acc = fo_node(a, c, lt, st, lv, acc, self);
+            a.cp[c] = acc;
+            a.ssel[c] = self;
+            c = c2;
+            lt = lt2;
+            st = st2;
+            lv = lv2;
+        }
+    }
+}
+
+// topmost self-selected cluster below the root on each chain: word (ancestor, best); the
+// ancestor is the cluster itself once the chain reaches the root's children
+__global__ void fo_sel_init(const int32_t *__restrict__ cpar, const int32_t *__restrict__ ssel,
+                            const int32_t *__restrict__ Kp, uint64_t *__restrict__ tw, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    const int32_t K = *Kp;
+    HDB_GRID_STRIDE(c, K) {
+        if (c == K - 1) {
+            tw[c] = pk((int32_t)c, NONE);
+            continue;
+        }
+        const int32_t p = cpar[c];
+        tw[c] = pk(p == K - 1 ? (int32_t)c : p, ssel[c] ? (int32_t)c : NONE);
+    }
+}
+
+__global__ void fo_sel_jump(uint64_t *__restrict__ tw, const int32_t *__restrict__ Kp, const int *__restrict__ flag_prev,
+                            int *__restrict__ flag_next, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    if (flag_prev && *flag_prev == 0) return;
+    const int32_t K = *Kp;
+    int ch = 0;
+    HDB_GRID_STRIDE(c, K) {
+        uint64_t w = tw[c];
+        bool moved = false;
+#pragma unroll 1
+        for (int it = 0; it < 3; it++) {  // several doublings per launch (fewer launches)
+            const int32_t x = pk_lo(w);
+            if (x == (int32_t)c) break;
+            const uint64_t w2 = tw[x];
+            const int32_t x2 = pk_lo(w2), v2 = pk_hi(w2);
+            w = pk(x2 == x ? (int32_t)c : x2, v2 != NONE ? v2 : pk_hi(w));
+            moved = true;
+        }
+        if (moved) {
+            tw[c] = w;
+            ch = 1;
+        }
+    }
+    flag_or(flag_next, ch);
+}
+
+// chosen = its own topmost self-selected ancestor-or-self; mark its smallest point id
+__global__ void fo_mark(const uint64_t *__restrict__ tw, const int32_t *__restrict__ cmin, const int32_t *__restrict__ Kp,
+                        int32_t *__restrict__ mk, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    const int32_t K = *Kp;
+    HDB_GRID_STRIDE(c, K - 1) {
+        if (pk_hi(tw[c]) == (int32_t)c) mk[cmin[c]] = 1;
+    }
+}
+
+__global__ void fo_labels(const uint64_t *__restrict__ tw, const int32_t *__restrict__ cmin,
+                          const int32_t *__restrict__ rk, const int32_t *__restrict__ Kp, int32_t *__restrict__ clab, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    const int32_t K = *Kp;
+    HDB_GRID_STRIDE(c, K) {
+        const int32_t v = pk_hi(tw[c]);
+        clab[c] = v == NONE ? 0 : rk[cmin[v]] + 1;
+    }
+}
+
+__global__ void fo_count(const int32_t *__restrict__ mk, const int32_t *__restrict__ rk, int64_t n,
+                         int64_t *__restrict__ out, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
+    if (threadIdx.x == 0 && blockIdx.x == 0) *out = (int64_t)rk[n - 1] + mk[n - 1];
+}
+
 // labels: a point's node -> its cluster (cs) -> the label of the nearest selected ancestor
-// cluster (propagated over the cluster tree on the host; 0 = none)
+// cluster (0 = none)
 __global__ void fl_point_labels(const int32_t *__restrict__ pparent, const int32_t *__restrict__ top,
                                 const int32_t *__restrict__ cs, const int32_t *__restrict__ cid,
-                                const int32_t *__restrict__ clab, int64_t n, int32_t *__restrict__ labels) {
+                                const int32_t *__restrict__ clab, int64_t n, int32_t *__restrict__ labels, const int *__restrict__ bad) {
+    if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
     HDB_GRID_STRIDE(v, n) labels[v] = clab[cid[cs[top[pparent[v]]]]];
 }
+
+// zero-initialised FOSC block: nch, kcur, plen, maxld (+ counters), pwide, a spare (m ints
+// each: 24m bytes, so the u64 array after them is 8-byte aligned), hkey (m u64), 192 jump flags
+inline size_t fz_layout(int64_t m) { return (size_t)m * 24 + (size_t)m * 8 + 192 * 4; }
 
 inline int grid_for(int64_t count) { return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(count, 256), 16384)); }
 
@@ -685,8 +1293,9 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     // ---- 2. Kruskal tree by rank divide and conquer
     int J = 0;
     while ((int64_t(1) << J) <= m) J++;  // 2^J > m: every rank < m has a clear bit below J
-    // global depths split blocks down to LOC_EDGES ranks; dc_local finishes each such block
-    for (int j = 0; j < J - LOC_LOG; j++) {
+    // global depths split blocks down to 2^LB ranks; dc_block (dc_local) finishes each such block
+    const int LB = ctx->flat_block_log >= 8 && ctx->flat_block_log <= 10 ? ctx->flat_block_log : LOC_LOG;
+    for (int j = 0; j < J - LB; j++) {
         const int b = J - 1 - j;
         // L ranks (bit b clear) below m; every U rank is an L rank + 2^b
         const int64_t blk = int64_t(1) << (b + 1), half = int64_t(1) << b;
@@ -697,7 +1306,13 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         hipLaunchKernelGGL(dc_root, dim3(gl), dim3(ROOT_TB), 0, st, dc, b, j, nl);
         hipLaunchKernelGGL(dc_link, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
     }
-    hipLaunchKernelGGL(dc_local, dim3((int)std::min<int64_t>(ceil_div(m, LOC_EDGES), 65536)), dim3(64), 0, st, dc, err);
+    const unsigned nblk = (unsigned)std::min<int64_t>(ceil_div(m, int64_t(1) << LB), 65536);
+    switch (ctx->flat_block_log) {
+    case 8: hipLaunchKernelGGL((dc_block<8, 128>), dim3(nblk), dim3(128), 0, st, dc, err); break;
+    case 9: hipLaunchKernelGGL((dc_block<9, 256>), dim3(nblk), dim3(256), 0, st, dc, err); break;
+    case 10: hipLaunchKernelGGL((dc_block<10, 512>), dim3(nblk), dim3(512), 0, st, dc, err); break;
+    default: hipLaunchKernelGGL(dc_local, dim3(nblk), dim3(64), 0, st, dc, err);
+    }
 
     // ---- 3. multi-way nodes, condensation
     // reuse the union-find scratch (n + m ints each) for the node arrays
@@ -717,6 +1332,11 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     nc2.take<int32_t>(m);  // clab
     nc2.take<int32_t>(64);  // jump flags
     nc2.take<int64_t>(1);  // cluster count
+    for (int k = 0; k < 11; k++) nc2.take<int32_t>(m);  // csz kstart kids pnodes poff ssel Kp rc rl mlist llist
+    for (int k = 0; k < 7; k++) nc2.take<uint64_t>(m);  // jw tw cpv lw rs mpre postv
+    nc2.take<char>(fz_layout(m));                        // zeroed block
+    nc2.take<int32_t>(n);                                // mk
+    nc2.take<int32_t>(n);                                // rk
     Carver cv2{(char *)arena(ctx, A_FLAT1, nc2.off), 0};
     int32_t *cs = cv2.take<int32_t>(m), *cid = cv2.take<int32_t>(m);
     uint64_t *key1 = cv2.take<uint64_t>(m), *key2 = cv2.take<uint64_t>(m);
@@ -725,8 +1345,24 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     double *stab = cv2.take<double>(m);
     int32_t *cpar = cv2.take<int32_t>(m), *cminid = cv2.take<int32_t>(m), *clab = cv2.take<int32_t>(m);
     int *jflags = cv2.take<int32_t>(64);
+    cv2.take<int64_t>(1);
+    int32_t *csz = cv2.take<int32_t>(m), *kstart = cv2.take<int32_t>(m), *kids = cv2.take<int32_t>(m),
+            *pnodes = cv2.take<int32_t>(m), *poff = cv2.take<int32_t>(m),
+            *ssel = cv2.take<int32_t>(m), *Kp = cv2.take<int32_t>(m), *rc = cv2.take<int32_t>(m),
+            *rl = cv2.take<int32_t>(m), *mlist = cv2.take<int32_t>(m), *llist = cv2.take<int32_t>(m);
+    uint64_t *jw = cv2.take<uint64_t>(m), *tw = cv2.take<uint64_t>(m);
+    double *cpv = cv2.take<double>(m);
+    uint64_t *lw = cv2.take<uint64_t>(m);
+    double *rs = cv2.take<double>(m), *mpre = cv2.take<double>(m), *postv = cv2.take<double>(m);
+    char *fz = cv2.take<char>(fz_layout(m));
+    const size_t fz_bytes = fz_layout(m);
+    int32_t *nch = (int32_t *)fz, *kcur = nch + m, *plen = kcur + m, *maxld = plen + m;  // (m ints)
+    int32_t *mcount = maxld + 1, *lcount = maxld + 2, *pwide = maxld + m;
+    unsigned long long *hkey = (unsigned long long *)(pwide + 2 * m);
+    int *ffl = (int *)(hkey + m);  // 192 jump flags
+    int32_t *mk = cv2.take<int32_t>(n), *rk = cv2.take<int32_t>(n);
     int rounds = 2;
-    for (int64_t span = 3; span < m; span *= 3) rounds++;
+    for (int64_t span = 9; span < m; span *= 9) rounds++;
     rounds = std::min(rounds, 64);
     auto jump_all = [&](int32_t *up) {  // roots of an upward forest, in place
         HIP_CHECK(hipMemsetAsync(jflags, 0, sizeof(int) * 64, st));
@@ -749,20 +1385,13 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         void *tmp = arena(ctx, A_FLAT_TMP, tb);
         HIP_CHECK(rocprim::exclusive_scan(tmp, tb, is_start, cid, 0, (size_t)m, rocprim::plus<int32_t>(), st));
     }
-    // the root (rank m-1) always starts a cluster: count = cid[m-1] + 1
-    HIP_CHECK(hipMemcpyAsync(pin, cid + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(pin + 1, err, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-    const int e1 = *(int *)(pin + 1);
-    if (e1 & FE_CYCLE) HDB_THROW(HDB_EINVAL, "flat labels: the edges contain a cycle");
-    if (e1 & FE_ROOTS) HDB_THROW(HDB_EINVAL, "flat labels: the edges are not a spanning tree");
-    const int32_t K = *(int32_t *)pin + 1;  // clusters incl. the root (cid K-1)
-
-    // ---- 4. stabilities: chains grouped by cluster, descending level inside
+    // ---- 4. stabilities: chains grouped by cluster, descending level inside.  The cluster
+    // count K stays on the device (no host round trip): kernels read it, and the key width
+    // is bounded by m (the same number of radix passes at every K of this size)
     hipLaunchKernelGGL(fl_terms, dim3(g), dim3(256), 0, st, top, pnode, cs, cid, dc.esize, nvalid, vsum, ew, m, mcs,
-                       key1, val1);
+                       key1, val1, err);
     int kb = 0;
-    while ((int64_t(1) << kb) < (int64_t)K + 1) kb++;
+    while ((int64_t(1) << kb) < m + 1) kb++;
     {
         size_t tb = 0;
         // keys of non-terms are all-ones: sorting on the cluster bits + 32 keeps them last
@@ -771,81 +1400,77 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         HIP_CHECK(sort_pairs(tmp, tb, key1, key2, val1, val2, m, 0, std::min(64, 32 + kb + 1), st));
     }
     int32_t *seg_hi = (int32_t *)key1;  // key1 is free after the sort
-    hipLaunchKernelGGL(fill_i32, dim3(grid_for(K)), dim3(256), 0, st, seg, K, -1);
-    hipLaunchKernelGGL(fl_seg, dim3(g), dim3(256), 0, st, key2, m, seg, seg_hi);
-    hipLaunchKernelGGL(fl_stab, dim3((int)std::min<int64_t>(K, 65536)), dim3(64), 0, st, val2, seg, seg_hi, K, stab);
-    hipLaunchKernelGGL(fl_cluster_meta, dim3(g), dim3(256), 0, st, is_start, cid, cs, pnode, dc.eminid, m, cpar, cminid);
-    // pinned staging: [stab K doubles][par K][min K][lab K]
-    char *hs = (char *)host_arena(ctx, (size_t)K * 20);
-    double *hstab = (double *)hs;
-    int32_t *hpar = (int32_t *)(hs + (size_t)K * 8), *hmin = hpar + K, *hlab = hmin + K;
-    HIP_CHECK(hipMemcpyAsync(hpar, cpar, sizeof(int32_t) * K, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(hmin, cminid, sizeof(int32_t) * K, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(hstab, stab, sizeof(double) * K, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-    const auto t_host0 = std::chrono::steady_clock::now();
-    std::fill(hlab, hlab + K, 0);
+    hipLaunchKernelGGL(fill_i32, dim3(g), dim3(256), 0, st, seg, m, -1);
+    hipLaunchKernelGGL(fl_seg, dim3(g), dim3(256), 0, st, key2, m, seg, seg_hi, err);
+    hipLaunchKernelGGL(fl_cluster_meta, dim3(g), dim3(256), 0, st, is_start, cid, cs, pnode, dc.eminid, dc.esize, m,
+                       cpar, cminid, csz, Kp, err);
+    hipLaunchKernelGGL(fl_stab, dim3((int)std::min<int64_t>(m, 16384)), dim3(64), 0, st, val2, seg, seg_hi, Kp, stab, err);
 
-    // FOSC (flat.cpp step 3) over the K clusters: ids ascend with the start node's rank, so a
-    // child cluster always precedes its parent; the root is K-1.  Scratch is per thread and
-    // reused (fresh pages cost more than the O(K) work).
-    static thread_local std::vector<int32_t> koff, kids, fillp, sel;
-    static thread_local std::vector<double> contrib;
-    static thread_local std::vector<char> flg;  // bit 0: self-selected, 1: chosen, 2: blocked
-    koff.assign((size_t)K + 1, 0);
-    kids.resize((size_t)K);
-    for (int32_t c = 0; c < K - 1; c++) koff[hpar[c] + 1]++;
-    for (int32_t c = 0; c < K; c++) koff[c + 1] += koff[c];
-    fillp.assign(koff.begin(), koff.end() - 1);
-    for (int32_t c = 0; c < K - 1; c++) kids[fillp[hpar[c]]++] = c;
-    contrib.resize((size_t)K);
-    flg.assign((size_t)K, 0);
-    const int32_t *kp = kids.data();
-    double *cp = contrib.data();
-    for (int32_t c = 0; c < K - 1; c++) {
-        const int32_t k0 = koff[c], k1 = koff[c + 1];
-        double prop = 0.0;
-        if (k1 - k0 == 2) {  // the common binary split: children summed in ascending smallest id
-            const int32_t a = kp[k0], b = kp[k0 + 1];
-            prop = hmin[a] < hmin[b] ? cp[a] + cp[b] : cp[b] + cp[a];
-        } else {
-            if (k1 - k0 > 2)
-                std::sort(kids.begin() + k0, kids.begin() + k1, [&](int32_t a, int32_t b) { return hmin[a] < hmin[b]; });
-            for (int32_t k = k0; k < k1; k++) prop = prop + cp[kp[k]];
-        }
-        if (k1 == k0 || hstab[c] >= prop) {  // Cluster.propagate: ties keep the parent
-            cp[c] = hstab[c];
-            flg[c] = 1;
-        } else {
-            cp[c] = prop;
-        }
+    // ---- 5. FOSC on the device (heavy-path walkers), selection, labels
+    int jrounds = 2;  // three doublings per launch: 8x reach per launch
+    for (int64_t reach = 1; reach < m; reach *= 8) jrounds++;
+    jrounds = std::min(jrounds, 64);
+    auto jump64 = [&](auto kern, uint64_t *wd, int *flags) {  // flags: jrounds ints, zeroed below
+        for (int k = 0; k < jrounds; k++)
+            hipLaunchKernelGGL(kern, dim3(g / 4 + 1), dim3(1024), 0, st, wd, Kp, k ? flags + k - 1 : nullptr, flags + k, err);
+    };
+    // zero: nch, kcur, plen, maxld, hkey (contiguous) and the jump flags
+    HIP_CHECK(hipMemsetAsync(fz, 0, fz_bytes, st));
+    hipLaunchKernelGGL(fo_children, dim3(g), dim3(256), 0, st, cpar, csz, Kp, nch, hkey, err);
+    {
+        size_t tb = 0;
+        HIP_CHECK(rocprim::exclusive_scan(nullptr, tb, nch, kstart, 0, (size_t)m, rocprim::plus<int32_t>(), st));
+        void *tmp = arena(ctx, A_FLAT_TMP, tb);
+        HIP_CHECK(rocprim::exclusive_scan(tmp, tb, nch, kstart, 0, (size_t)m, rocprim::plus<int32_t>(), st));
     }
-    // selected = self-selected with no selected ancestor below the root (top-down = descending id)
-    sel.clear();
-    for (int32_t c = K - 2; c >= 0; c--) {
-        const int32_t p = hpar[c];
-        const bool blocked = p != K - 1 && (flg[p] & 6);
-        if (blocked) flg[c] |= 4;
-        else if (flg[c] & 1) {
-            flg[c] |= 2;
-            sel.push_back(c);
-        }
+    hipLaunchKernelGGL(fo_kids_fill, dim3(g), dim3(256), 0, st, cpar, Kp, kstart, kcur, kids, err);
+    hipLaunchKernelGGL(fo_paths_init, dim3(g), dim3(256), 0, st, cpar, cminid, Kp, nch, hkey, kstart, kids, jw, err);
+    jump64(fo_jump_sum, jw, ffl);
+    hipLaunchKernelGGL(fo_paths_meta, dim3(g), dim3(256), 0, st, cpar, Kp, nch, jw, plen, lw, err);
+    jump64(fo_jump_sum, lw, ffl + 128);
+    {
+        size_t tb = 0;
+        HIP_CHECK(rocprim::exclusive_scan(nullptr, tb, plen, poff, 0, (size_t)m, rocprim::plus<int32_t>(), st));
+        void *tmp = arena(ctx, A_FLAT_TMP, tb);
+        HIP_CHECK(rocprim::exclusive_scan(tmp, tb, plen, poff, 0, (size_t)m, rocprim::plus<int32_t>(), st));
     }
-    std::sort(sel.begin(), sel.end(), [&](int32_t a, int32_t b) { return hmin[a] < hmin[b]; });
-    for (size_t i = 0; i < sel.size(); i++) hlab[sel[i]] = (int32_t)(i + 1);
-    // every cluster takes the label of its nearest selected ancestor-or-self; the root keeps 0
-    for (int32_t c = K - 2; c >= 0; c--)
-        if (hlab[c] == 0) hlab[c] = hlab[hpar[c]];
-    ctx->stats["flat_host_us"] =
-        std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t_host0).count();
-    HIP_CHECK(hipMemcpyAsync(clab, hlab, sizeof(int32_t) * K, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(fo_paths_nodes, dim3(g), dim3(256), 0, st, Kp, jw, poff, lw, pnodes, maxld, err);
+    hipLaunchKernelGGL(fo_paths_rec, dim3(g), dim3(256), 0, st, Kp, pnodes, nch, hkey, kstart, kids, stab, rc, rl, rs,
+                       mlist, mcount, jw, pwide, err);
+    hipLaunchKernelGGL(fo_long_list, dim3(g), dim3(256), 0, st, Kp, jw, plen, pwide, llist, lcount, err);
+    FoscArr fa{cpar, nch, kstart, kids, plen, poff, rc, rl, Kp, mlist, mcount, pwide, llist, lcount, rs, jw, lw, hkey,
+               maxld, ssel, csz /* free after fo_children: heavy positions */, cpv, mpre, postv};
+    // a light child has at most half its parent's points: light depth <= log2(n)
+    int dmax = 0;
+    while ((int64_t(1) << (dmax + 1)) <= n) dmax++;
+    for (int d = dmax; d >= 0; d--) {
+        hipLaunchKernelGGL(fo_multi_pre, dim3(1024), dim3(64), 0, st, fa, d, err);
+        hipLaunchKernelGGL(fo_walk, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(m, 64), 8192))),
+                           dim3(64), 0, st, fa, d, err);
+    }
+    hipLaunchKernelGGL(fo_sel_init, dim3(g), dim3(256), 0, st, cpar, ssel, Kp, tw, err);
+    jump64(fo_sel_jump, tw, ffl + 64);
+    HIP_CHECK(hipMemsetAsync(mk, 0, sizeof(int32_t) * n, st));
+    hipLaunchKernelGGL(fo_mark, dim3(g), dim3(256), 0, st, tw, cminid, Kp, mk, err);
+    {
+        size_t tb = 0;
+        HIP_CHECK(rocprim::exclusive_scan(nullptr, tb, mk, rk, 0, (size_t)n, rocprim::plus<int32_t>(), st));
+        void *tmp = arena(ctx, A_FLAT_TMP, tb);
+        HIP_CHECK(rocprim::exclusive_scan(tmp, tb, mk, rk, 0, (size_t)n, rocprim::plus<int32_t>(), st));
+    }
+    hipLaunchKernelGGL(fo_labels, dim3(g), dim3(256), 0, st, tw, cminid, rk, Kp, clab, err);
+    hipLaunchKernelGGL(fo_count, dim3(1), dim3(64), 0, st, mk, rk, n, (int64_t *)(words + 3), err);
     hipLaunchKernelGGL(fl_point_labels, dim3(grid_for(n)), dim3(256), 0, st, pparent, top, cs, cid, clab, n,
-                       labels);
+                       labels, err);
     HIP_CHECK(hipGetLastError());
-    // the pinned staging is rewritten by the next call: wait for the queued copy
+    HIP_CHECK(hipMemcpyAsync(pin, words, sizeof(int64_t) * 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(pin + 4, Kp, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    if (n_clusters) *n_clusters = (int64_t)sel.size();
-    ctx->stats["flat_clusters_total"] = K;  // condensed-tree clusters incl. the root
+    const int e1 = (int)pin[1];
+    if (e1 & FE_CYCLE) HDB_THROW(HDB_EINVAL, "flat labels: the edges contain a cycle");
+    if (e1 & FE_ROOTS) HDB_THROW(HDB_EINVAL, "flat labels: the edges are not a spanning tree");
+    if (n_clusters) *n_clusters = pin[3];
+    ctx->stats["flat_clusters_total"] = *(int32_t *)(pin + 4);  // condensed-tree clusters incl. the root
 }
 
 }  // namespace hdb

@@ -36,6 +36,102 @@ __global__ void edge_gather_kernel(const int32_t *__restrict__ perm, int64_t ne,
     }
 }
 
+// --- run-aware merge.  The exact leaf hands over its n-1 tree edges ascending by (w, lo, hi)
+// followed by n self edges in id order, and the reducers' concatenations keep such runs: a
+// non-decreasing prefix P (length p) and a rest R.  The stable descending order of P ++ R is
+// then: R radix-sorted alone (stable, descending), P reversed tie group by tie group (equal
+// weights keep their input order), and the two merged with P first on equal weights --
+// output position of P[i] = its place in reversed P + #(R > w_i), of R'[j] = j + #(P >= w).
+// Both counts are binary searches in sorted arrays.  Identical to the full stable sort.
+// first descent f (w[f-1] > w[f]) kept as ne - f by atomicMax on a zeroed word
+__global__ void run_scan_kernel(const double *__restrict__ w, int64_t ne, int64_t *__restrict__ first_desc,
+                                int *__restrict__ nan) {
+    int64_t f = ne;
+    int bad = 0;
+    HDB_GRID_STRIDE(i, ne) {
+        const double a = w[i];
+        if (a != a) bad = 1;
+        if (i + 1 < ne && a > w[i + 1]) f = min(f, i + 1);
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        f = min(f, (int64_t)__shfl_xor((long long)f, o));
+        bad |= __shfl_xor(bad, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (f < ne) atomicMax((unsigned long long *)first_desc, (unsigned long long)(ne - f));
+        if (bad) atomicOr(nan, 1);
+    }
+}
+
+__global__ void run_keys_kernel(const double *__restrict__ w, int64_t p, int64_t r, double *__restrict__ keys,
+                                int32_t *__restrict__ iota) {
+    HDB_GRID_STRIDE(j, r) {
+        const double x = w[p + j];
+        keys[j] = (x == 0.0) ? 0.0 : x;
+        iota[j] = (int32_t)(p + j);
+    }
+}
+
+// first index in ascending a[0, n) with a[k] >= x (k = n: none)
+__device__ __forceinline__ int64_t lower_bound_asc(const double *a, int64_t n, double x) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int64_t upper_bound_asc(const double *a, int64_t n, double x) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] <= x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+// first index in descending a[0, n) with a[k] <= x = #(a > x)
+__device__ __forceinline__ int64_t count_greater_desc(const double *a, int64_t n, double x) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] > x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void run_place_p_kernel(const int32_t *__restrict__ va, const int32_t *__restrict__ vb,
+                                   const double *__restrict__ w, int64_t p, const double *__restrict__ rkeys, int64_t r,
+                                   int32_t *__restrict__ oa, int32_t *__restrict__ ob, double *__restrict__ ow) {
+    HDB_GRID_STRIDE(i, p) {
+        const double x = w[i];
+        int64_t gs = i, ge = i + 1;
+        if ((i > 0 && w[i - 1] == x) || (i + 1 < p && w[i + 1] == x)) {  // a tie group (rare)
+            gs = lower_bound_asc(w, p, x);
+            ge = upper_bound_asc(w, p, x);
+        }
+        const int64_t o = (p - ge) + (i - gs) + count_greater_desc(rkeys, r, x);
+        oa[o] = va[i];
+        ob[o] = vb[i];
+        ow[o] = x;
+    }
+}
+
+__global__ void run_place_r_kernel(const int32_t *__restrict__ va, const int32_t *__restrict__ vb,
+                                   const double *__restrict__ w, int64_t p, const double *__restrict__ rkeys,
+                                   const int32_t *__restrict__ rperm, int64_t r, int32_t *__restrict__ oa,
+                                   int32_t *__restrict__ ob, double *__restrict__ ow) {
+    HDB_GRID_STRIDE(j, r) {
+        const int32_t s = rperm[j];
+        const int64_t o = j + (p - lower_bound_asc(w, p, rkeys[j]));
+        oa[o] = va[s];
+        ob[o] = vb[s];
+        ow[o] = w[s];
+    }
+}
+
 // in-place stable descending sort of (va, vb, w)
 void sort_edges_desc_device(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne) {
     if (ne <= 1) return;
@@ -48,23 +144,52 @@ void sort_edges_desc_device(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, i
     };
     size_t o_k = carve(sizeof(double) * ne), o_k2 = carve(sizeof(double) * ne), o_i = carve(sizeof(int32_t) * ne),
            o_p = carve(sizeof(int32_t) * ne), o_a = carve(sizeof(int32_t) * ne), o_b = carve(sizeof(int32_t) * ne),
-           o_w = carve(sizeof(double) * ne);
+           o_w = carve(sizeof(double) * ne), o_x = carve(sizeof(int64_t) * 2);
     char *base = (char *)arena(ctx, A_WORK3, off);
     double *keys = (double *)(base + o_k), *keys2 = (double *)(base + o_k2);
     int32_t *iota = (int32_t *)(base + o_i), *perm = (int32_t *)(base + o_p);
     int32_t *ta = (int32_t *)(base + o_a), *tb_ = (int32_t *)(base + o_b);
     double *tw = (double *)(base + o_w);
+    int64_t *xw = (int64_t *)(base + o_x);
     int g = (int)std::min<int64_t>(ceil_div(ne, 256), 8192);
+    hipStream_t st = ctx->stream;
     KernelTimer t(ctx, "merge_sort");
-    hipLaunchKernelGGL(edge_keys_kernel, dim3(g), dim3(256), 0, ctx->stream, w, ne, keys, iota);
-    size_t tb = 0;
-    HIP_CHECK(sort_pairs_desc(nullptr, tb, keys, keys2, iota, perm, ne, 0, 64, ctx->stream));
-    void *tmp = arena(ctx, A_SORT, tb);
-    HIP_CHECK(sort_pairs_desc(tmp, tb, keys, keys2, iota, perm, ne, 0, 64, ctx->stream));
-    hipLaunchKernelGGL(edge_gather_kernel, dim3(g), dim3(256), 0, ctx->stream, perm, ne, va, vb, w, ta, tb_, tw);
-    HIP_CHECK(hipMemcpyAsync(va, ta, sizeof(int32_t) * ne, hipMemcpyDeviceToDevice, ctx->stream));
-    HIP_CHECK(hipMemcpyAsync(vb, tb_, sizeof(int32_t) * ne, hipMemcpyDeviceToDevice, ctx->stream));
-    HIP_CHECK(hipMemcpyAsync(w, tw, sizeof(double) * ne, hipMemcpyDeviceToDevice, ctx->stream));
+    int64_t p = 0;
+    if (ctx->merge_runs && ne >= 4096) {
+        int64_t *pin = pinned_words(ctx) + PINNED_WORDS - 16;  // private slice
+        HIP_CHECK(hipMemsetAsync(xw, 0, sizeof(int64_t) * 2, st));
+        hipLaunchKernelGGL(run_scan_kernel, dim3(g), dim3(256), 0, st, w, ne, xw, (int *)(xw + 1));
+        HIP_CHECK(hipMemcpyAsync(pin, xw, sizeof(int64_t) * 2, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        const int64_t pre = ne - pin[0];  // the device keeps ne - (first descent), 0: none
+        // a short prefix does not pay for the extra pass; NaN keys keep the radix order
+        if (pin[1] == 0 && pre >= ne / 4) p = pre;
+    }
+    if (p > 0) {
+        const int64_t r = ne - p;
+        if (r > 0) {
+            const int gr = (int)std::min<int64_t>(ceil_div(r, 256), 8192);
+            hipLaunchKernelGGL(run_keys_kernel, dim3(gr), dim3(256), 0, st, w, p, r, keys, iota);
+            size_t tb = 0;
+            HIP_CHECK(sort_pairs_desc(nullptr, tb, keys, keys2, iota, perm, r, 0, 64, st));
+            void *tmp = arena(ctx, A_SORT, tb);
+            HIP_CHECK(sort_pairs_desc(tmp, tb, keys, keys2, iota, perm, r, 0, 64, st));
+            hipLaunchKernelGGL(run_place_r_kernel, dim3(gr), dim3(256), 0, st, va, vb, w, p, keys2, perm, r, ta, tb_,
+                               tw);
+        }
+        hipLaunchKernelGGL(run_place_p_kernel, dim3((int)std::min<int64_t>(ceil_div(p, 256), 8192)), dim3(256), 0, st,
+                           va, vb, w, p, keys2, r, ta, tb_, tw);
+    } else {
+        hipLaunchKernelGGL(edge_keys_kernel, dim3(g), dim3(256), 0, st, w, ne, keys, iota);
+        size_t tb = 0;
+        HIP_CHECK(sort_pairs_desc(nullptr, tb, keys, keys2, iota, perm, ne, 0, 64, st));
+        void *tmp = arena(ctx, A_SORT, tb);
+        HIP_CHECK(sort_pairs_desc(tmp, tb, keys, keys2, iota, perm, ne, 0, 64, st));
+        hipLaunchKernelGGL(edge_gather_kernel, dim3(g), dim3(256), 0, st, perm, ne, va, vb, w, ta, tb_, tw);
+    }
+    HIP_CHECK(hipMemcpyAsync(va, ta, sizeof(int32_t) * ne, hipMemcpyDeviceToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(vb, tb_, sizeof(int32_t) * ne, hipMemcpyDeviceToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(w, tw, sizeof(double) * ne, hipMemcpyDeviceToDevice, st));
     HIP_CHECK(hipGetLastError());
 }
 

@@ -97,19 +97,31 @@ class MRHDBSCANStar:
         self.group = group      # torch.distributed group (None: the default group, if any)
         self._comm = None       # HdbComm for the merge under nccl
         self.timings = {}
+        self.level_tasks = []   # profile: per level, task durations + phase wall times
+        self._lvl = None
         self._t0 = None
         self._progress = bool(os.environ.get("HDB_PROGRESS"))  # one stderr line per level
 
     def _mark(self, phase):
+        """profile: phase wall time since the previous mark (synchronising); returns it"""
         if not self.profile:
-            return
+            return 0.0
         import time
         import torch
         torch.cuda.synchronize(self.device)
         now = time.perf_counter()
+        dt = 0.0
         if self._t0 is not None and phase:
-            self.timings[phase] = self.timings.get(phase, 0.0) + (now - self._t0)
+            dt = now - self._t0
+            self.timings[phase] = self.timings.get(phase, 0.0) + dt
         self._t0 = now
+        return dt
+
+    def _task(self, kind, weight, seconds):
+        """profile: one task's duration in the current level (the LPT weight the sharded
+        driver assigns it by, and its measured seconds at this world size)"""
+        if self.profile and self._lvl is not None:
+            self._lvl.setdefault(kind, []).append((float(weight), float(seconds)))
 
     # ------------------------------------------------------------------ helpers
     def _c(self):
@@ -140,9 +152,19 @@ class MRHDBSCANStar:
             va = torch.empty(ne, dtype=torch.int32, device=X.device)
             vb = torch.empty_like(va)
             w = torch.empty(ne, dtype=torch.float64, device=X.device)
+            if self.profile:
+                import time
+                torch.cuda.synchronize(X.device)
+                t_small = time.perf_counter()
             A.check(A.lib().hdb_leaf_msts(c.h, Xl.data_ptr(), offs.ctypes.data, len(small), X.shape[1],
                                           ids.data_ptr(), self.minPts, self.metric, core.data_ptr(), va.data_ptr(),
                                           vb.data_ptr(), w.data_ptr()), "FirstStep.leaf")
+            if self.profile:  # one batched launch: its time split over the leaves by n^2
+                torch.cuda.synchronize(X.device)
+                t_small = time.perf_counter() - t_small
+                wsum = float(np.sum(sizes.astype(np.float64) ** 2))
+                for sz in sizes.tolist():
+                    self._task("leaves", float(sz) ** 2, t_small * float(sz) ** 2 / wsum)
             eo = np.zeros(len(small) + 1, np.int64)
             eo[1:] = np.cumsum(2 * sizes - 1)
             by_key = {k: (va[eo[i]:eo[i + 1]], vb[eo[i]:eo[i + 1]], w[eo[i]:eo[i + 1]])
@@ -164,13 +186,16 @@ class MRHDBSCANStar:
             torch.cuda.current_stream(X.device).synchronize()  # inputs ready for the other streams
 
         def leaf(k, threaded):
+            import time
+            t0 = time.perf_counter()
             r, Xl, va, vb, w = jobs[k]
             cc = A.Context.get(self.device) if threaded else c
             A.check(A.lib().hdb_exact_mst(cc.h, Xl.data_ptr(), r.shape[0], X.shape[1], self.minPts, self.metric,
                                           A.CORE_INCL_SELF_CUMULATIVE, 1, None, va.data_ptr(), vb.data_ptr(),
                                           w.data_ptr()), "leaf exact MST")
-            if threaded:
+            if threaded or self.profile:
                 cc.synchronize()
+            self._task("leaves", float(r.shape[0]) ** 2, time.perf_counter() - t0)
 
         if len(big) > 1 and self.model_threads > 1:
             if self._pool is None:
@@ -199,6 +224,8 @@ class MRHDBSCANStar:
         n, d = X.shape
         c = self._c()
         self.timings = {}
+        self.level_tasks = []
+        self._lvl = None
         self._t0 = None
         self._mark(None)
         import time
@@ -229,6 +256,9 @@ class MRHDBSCANStar:
                     big.append((kk, s0, cnt))
             level = dict(iteration=iteration, leaves={k: int(r.shape[0]) for k, r in zip(leaf_k, leaf_rows)},
                          big={k: cnt for k, _, cnt in big}, labels={}, new_keys={})
+            if self.profile:
+                self._lvl = {"phase_s": {}}
+                self.level_tasks.append(self._lvl)
             if leaf_k:
                 self._mark("bookkeeping")
                 owner = P.lpt([int(r.shape[0]) ** 2 for r in leaf_rows], world)
@@ -238,7 +268,8 @@ class MRHDBSCANStar:
                     blocks.extend(((iteration, 0, i), e) for i, e in zip(mine, got))
                 for i, r in enumerate(leaf_rows):
                     block_size[(iteration, 0, i)] = 2 * int(r.shape[0]) - 1
-                self._mark("leaves")
+                if self.profile:
+                    self._lvl["phase_s"]["leaves"] = self._mark("leaves")
                 for kk, r in zip(leaf_k, leaf_rows):
                     leaf_of[r] = kk
             iteration += 1
@@ -275,7 +306,8 @@ class MRHDBSCANStar:
                                                    nearest.data_ptr(), None), "FirstStep.nearest")
             if world > 1:
                 nearest = P.allgather_var(nearest, self.group)
-            self._mark("nearest_sample")
+            if self.profile:
+                self._lvl["phase_s"]["nearest_sample"] = self._mark("nearest_sample")
             # nearest is the list position in S (keyed: within the point's own subset)
             nb = S.shape[0]
             ls = torch.empty((nb, d), dtype=torch.float64, device=dev)
@@ -285,13 +317,22 @@ class MRHDBSCANStar:
                                              A.BUBBLE_COMBINESTEP, ls.data_ptr(), ss.data_ptr(), rep.data_ptr(),
                                              info.data_ptr()), "CombineStep")
             rep_h, info_h = rep.cpu().numpy(), info.cpu().numpy()
-            self._mark("bubbles")
+            if self.profile:
+                self._lvl["phase_s"]["bubbles"] = self._mark("bubbles")
             s_gid_h = s_gid.cpu().numpy()
             new_key_of_bubble = np.full(nb, -2, np.int64)
             # local models: LPT over the ranks on b^2, results gathered, applied in subset order
             nonempty_of = [np.nonzero(info_h[s_off[i]:s_off[i + 1], 2] > 0)[0] for i in range(len(big))]  # D4
             owner = P.lpt([int(ne.shape[0]) ** 2 for ne in nonempty_of], world)
             def model(i):
+                import time
+                t0 = time.perf_counter()
+                try:
+                    return model_body(i)
+                finally:
+                    self._task("local_models", float(nonempty_of[i].shape[0]) ** 2, time.perf_counter() - t0)
+
+            def model_body(i):
                 a, b = s_off[i], s_off[i + 1]
                 nonempty = nonempty_of[i]
                 if nonempty.shape[0] < 2:
@@ -347,7 +388,8 @@ class MRHDBSCANStar:
                     forced.add(nk[0])  # D9
                 new_key_of_bubble[a + nonempty] = labels
             # LabelClassification.java:21-37 (bubble of the point -> relabelled label)
-            self._mark("local_models")
+            if self.profile:
+                self._lvl["phase_s"]["local_models"] = self._mark("local_models")
             tbl = torch.from_numpy(new_key_of_bubble).to(dev)
             key_of[brows] = tbl[nearest.long()]
             alive = brows

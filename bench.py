@@ -302,6 +302,44 @@ def partitioned_cpu_baseline(workload):
                       f"processing_units {cs['processing_units']}: {r['iterations']} levels in {dt:.1f} s"}
 
 
+def predicted_scaling(drv, par, ns=(1, 2, 4, 8)):
+    """C3/C5 --phases: the sharded driver's critical path at N ranks predicted from the tasks
+    measured at N = 1.  Per level: leaves and local models are assigned to ranks by the
+    driver's own LPT on its own weights (n^2, b^2); a rank's phase time = the summed measured
+    durations of its tasks x (phase wall time / summed task time at N = 1: the concurrency the
+    model threads reach on one GPU), the phase = its slowest rank; the point-chunked nearest
+    sample scales as 1/N; bubbles (recomputed on every rank), bookkeeping, the merge and the
+    flat labels do not scale.  Not modelled: the all-gathers and the RCCL merge exchange."""
+    fixed = sum(v for k, v in drv.timings.items() if k in ("bookkeeping", "merge", "flat_labels"))
+    out, per = {}, {}
+    for N in ns:
+        tot = {"leaves": 0.0, "local_models": 0.0, "nearest_sample": 0.0, "bubbles": 0.0}
+        for L in drv.level_tasks:
+            ph = L["phase_s"]
+            for kind in ("leaves", "local_models"):
+                tasks = L.get(kind, [])
+                wall = ph.get(kind, 0.0)
+                work = sum(t for _, t in tasks)
+                if not tasks or work <= 0:
+                    tot[kind] += wall
+                    continue
+                owner = par.lpt([w for w, _ in tasks], N)
+                load = np.zeros(N)
+                for (w, t), o in zip(tasks, owner):
+                    load[o] += t
+                tot[kind] += float(load.max()) * wall / work
+            tot["nearest_sample"] += ph.get("nearest_sample", 0.0) / N
+            tot["bubbles"] += ph.get("bubbles", 0.0)
+        per[N] = {k: round(v, 3) for k, v in tot.items()} | {"fixed": round(fixed, 3)}
+        out[N] = sum(tot.values()) + fixed
+    return {"model": "LPT makespan of the measured N=1 task durations per level (leaves, local models), "
+                     "nearest sample / N, bubbles + bookkeeping + merge + flat labels unscaled; "
+                     "all-gathers and the RCCL merge exchange not modelled",
+            "seconds": {str(N): round(v, 3) for N, v in out.items()},
+            "speedup": {str(N): round(out[1] / v, 2) for N, v in out.items()},
+            "phases": {str(N): v for N, v in per.items()}}
+
+
 def run_partitioned(args, workload):
     """C3 / C5: the whole MR-HDBSCAN* job (every level, the merge, the flat labels) on N GPUs
     with the sharded driver; every rank holds the parsed points (pinned host memory), the
@@ -406,6 +444,8 @@ def run_partitioned(args, workload):
                 "kernels_s": {k: round(v[0] / args.steps, 4) for k, v in sorted(kt.items(), key=lambda x: -x[1][0])},
                 "kernel_launches": {k: v[1] // args.steps for k, v in kt.items()},
                 "prim_coop_plain_retries": coop_retries,
+                "predicted_scaling": predicted_scaling(drv, importlib.import_module(PKG + ".parallel"))
+                if args.phases and world == 1 else None,
                 "roofline": partitioned_roofline(kt, coop_steps, coop_launches, args.steps)}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = partitioned_cpu_baseline(workload)

@@ -112,3 +112,33 @@ def test_device_exact_mst_blobs_and_skin_equal_host(pkg, ctx):
         t_host = time.perf_counter() - t0
         print(f"flat labels n={X.shape[0]}: device {t_dev * 1e3:.2f} ms, host {t_host * 1e3:.1f} ms, K={kg}")
         assert kg == kr and np.array_equal(got.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("teeth,tie", [(3000, 1), (3000, 3), (700, 7)])
+def test_device_comb_cluster_tree_equal_host(pkg, ctx, teeth, tie):
+    """a comb: spine edges of increasing weight (`tie` consecutive ones equal: multi-way splits),
+    a tooth of 5 points at every spine vertex (tight or loose) -- the condensed tree is a
+    caterpillar thousands of clusters high (FOSC heavy paths much longer than a wave's chunk)"""
+    rng = np.random.default_rng(teeth + tie)
+    va, vb, w = [], [], []
+    tooth = 5
+    for i in range(teeth):
+        base = i * tooth
+        loose = float(1 + i // tie) * rng.uniform(0.001, 1.5)  # some teeth dissolve first
+        for j in range(1, tooth):
+            va.append(base)
+            vb.append(base + j)
+            w.append(loose * rng.random())
+        if i:
+            va.append(base - tooth)
+            vb.append(base)
+            w.append(float(1 + (i - 1) // tie) + (0.5 * rng.random() if tie == 1 else 0.0))
+    n = teeth * tooth
+    va, vb, w = np.array(va, np.int32), np.array(vb, np.int32), np.array(w)
+    perm = rng.permutation(n).astype(np.int32)
+    va, vb = perm[va], perm[vb]
+    d = np.argsort(-w, kind="stable")
+    for mcs in (2, 4, 5, 6):
+        ref, kr = lib_flat(pkg, va[d], vb[d], w[d], n, mcs)
+        got, kg = dev_flat(pkg, ctx, va[d], vb[d], w[d], n, mcs)
+        assert kg == kr and np.array_equal(got, ref), (teeth, tie, mcs)

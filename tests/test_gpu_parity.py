@@ -6,6 +6,7 @@ for the CF variant's real-exponent Math.pow (ClusterFeatureDataBubbles.java:213)
 """
 import numpy as np
 import pytest
+import torch
 
 from conftest import blobs, golden, load_iris, load_skin
 
@@ -368,6 +369,51 @@ def test_sort_edges_desc_large_stable(pkg, oracle):
     ga, gb, gw = pkg.sort_edges_desc(a.copy(), b.copy(), w.copy())
     ra, rb, rw = oracle.merge_edges([(a, b, w)])
     assert eq(ga, ra) and eq(gb, rb) and eq(gw, rw)
+
+
+@pytest.mark.parametrize("p,r,levels", [(200_000, 200_001, 40), (300_000, 0, 7), (100_000, 290_000, 0),
+                                         (60_000, 180_000, 3), (5_000, 20_000, 2)])
+def test_sort_edges_desc_runs(pkg, oracle, p, r, levels):
+    """the run-aware merge (non-decreasing prefix + radix-sorted rest, merged): a prefix with
+    heavy tie groups (levels > 0: weights on a grid, incl. -0.0 next to +0.0), a rest that ties
+    with it, no rest at all, and a prefix below the run threshold -- equal to the oracle's
+    stable sort"""
+    rng = np.random.default_rng(p + r)
+    if levels:
+        pw = np.sort(rng.integers(0, levels + 1, p)).astype(np.float64) * 0.5
+    else:
+        pw = np.sort(rng.uniform(0, 50, p))
+    pw[pw == 0] = np.where(rng.random((pw == 0).sum()) < 0.5, -0.0, 0.0)
+    rw = rng.integers(0, max(levels, 1) + 1, r) * 0.5 if levels else rng.uniform(0, 50, r)
+    w = np.r_[pw, rw]
+    a = rng.integers(0, 1 << 30, p + r).astype(np.int32)
+    b = rng.integers(0, 1 << 30, p + r).astype(np.int32)
+    for dev in (False, True):
+        args = (a.copy(), b.copy(), w.copy())
+        if dev:
+            args = tuple(torch.from_numpy(x).cuda() for x in args)
+        ga, gb, gw = pkg.sort_edges_desc(*args)
+        if dev:
+            ga, gb, gw = (x.cpu().numpy() for x in (ga, gb, gw))
+        ra, rb, rw2 = oracle.merge_edges([(a, b, w)])
+        assert eq(ga, ra) and eq(gb, rb) and eq(gw, rw2) and np.array_equal(np.signbit(gw), np.signbit(rw2))
+
+
+def test_sort_edges_desc_exact_mst_list_and_nan(pkg, oracle):
+    """the exact leaf's own output (tree edges ascending, then self edges) and a NaN weight
+    (the run path is skipped: the radix order of NaN keys is kept)"""
+    X = np.random.default_rng(4).normal(size=(50_000, 3))
+    star = pkg.HDBSCANStar(pkg.Context.get(0))
+    _, g = star.exactMST(torch.from_numpy(X).cuda(), 4, None, 2, selfEdges=True)
+    a, b, w = (x.cpu().numpy() for x in (g.getVerticeA(), g.getVericeB(), g.getEges()))
+    ga, gb, gw = pkg.sort_edges_desc(a.copy(), b.copy(), w.copy())
+    ra, rb, rw = oracle.merge_edges([(a, b, w)])
+    assert eq(ga, ra) and eq(gb, rb) and eq(gw, rw)
+    w2 = w.copy()
+    w2[len(w2) // 2] = np.nan
+    ga, gb, gw = pkg.sort_edges_desc(a.copy(), b.copy(), w2.copy())
+    ha, hb, hw = pkg.sort_edges_desc(a.copy(), b.copy(), w2.copy())  # deterministic
+    assert eq(ga, ha) and eq(gb, hb) and np.isnan(gw).sum() == 1
 
 
 # -------------------------------------------------------------------- errors
