@@ -105,7 +105,7 @@ def lib():
             "hdb_quicksort_edges": [ip, ip, dp, i64],
             "hdb_sort_edges_desc": [vp, ip, ip, dp, i64],
             "hdb_flat_labels": [vp, ip, ip, dp, i64, i64, i32, ip, lp],
-            "hdb_local_mst_ids": [vp, ip, i64, ip, ip, i64, i32, ip, ip, ip],
+            "hdb_local_mst_ids": [vp, ip, i64, ip, ip, dp, i64, i32, ip, ip, ip],
             "hdb_comm_unique_id": [vp, i32],
             "hdb_comm_init": [vp, i32, i32, vp, C.POINTER(vp)],
             "hdb_free": [vp],

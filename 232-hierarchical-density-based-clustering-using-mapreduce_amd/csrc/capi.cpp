@@ -422,15 +422,16 @@ int hdb_sort_edges_desc(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64
     });
 }
 
-int hdb_local_mst_ids(hdb_ctx *ctx, const int32_t *ids, int64_t n, const int32_t *va, const int32_t *vb, int64_t ne,
-                      int32_t node, int32_t *fake1, int32_t *fake2, int32_t *node_out) {
+int hdb_local_mst_ids(hdb_ctx *ctx, const int32_t *ids, int64_t n, const int32_t *va, const int32_t *vb,
+                      const double *w, int64_t ne, int32_t node, int32_t *fake1, int32_t *fake2, int32_t *node_out) {
     return guarded(ctx, [&] {
         if (n < 0 || ne < 0 || (ne > 0 && (!va || !vb || !fake1 || !fake2))) HDB_THROW(HDB_EINVAL, "bad arguments");
         Stager sg(ctx);
         const int32_t *di = sg.in(ids, (size_t)n);
         const int32_t *da = sg.in(va, (size_t)ne), *db = sg.in(vb, (size_t)ne);
+        const double *dw = sg.in(w, (size_t)ne);
         int32_t *f1 = sg.out(fake1, (size_t)ne), *f2 = sg.out(fake2, (size_t)ne), *nd = sg.out(node_out, (size_t)ne);
-        local_mst_ids_device(ctx, di, n, da, db, ne, node, f1, f2, nd);
+        local_mst_ids_device(ctx, di, n, da, db, dw, ne, node, f1, f2, nd);
         sg.finish();
     });
 }

@@ -82,6 +82,7 @@ struct hdb_ctx {
     int prim_coop_slots = 4;  // cooperative Prim exchange, rows in registers (d <= 16): 1 release/acquire slots, 2 granules,
                               // 3 drained sc1 slots, 4 DPP folds + key granules (default), 5 key+row granule sweep
     bool merge_runs = false;   // merge sort: radix-sort only what follows a non-decreasing prefix, then merge (slower as built: sync + binary searches)
+    int flat_root_variant = 3;  // K6 dc_root A/B: 0 LDS table (256 threads), 1 (1024), 2 direct atomics, 3-5 multi-batch
     int flat_block_log = 10;   // K6: deep depths per workgroup in LDS (2^x ranks, 8-10; 0: the sequential dc_local)
     bool count_evals = false;  // K1t counts evaluated pairs (diagnostic; costs one sync)
     std::map<std::string, int64_t> stats;  // diagnostic counters (count_evals)

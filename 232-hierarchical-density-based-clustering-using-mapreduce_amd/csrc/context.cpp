@@ -165,6 +165,7 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         // per-kernel HIP-event timing from birth (contexts created on worker threads, bench.py)
         if (const char *e = getenv("HDB_KERNEL_TIMING")) c->timing = atoi(e) != 0;
         if (const char *e = getenv("HDB_FLAT_BLOCK_LOG")) c->flat_block_log = atoi(e);  // A/B knob
+        if (const char *e = getenv("HDB_FLAT_ROOT")) c->flat_root_variant = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_MERGE_RUNS")) c->merge_runs = atoi(e) != 0;      // A/B knob
         *out = c;
         return HDB_OK;

@@ -259,11 +259,12 @@ __device__ __forceinline__ int32_t wave_sum(int32_t v) {
 // in an LDS table keyed by representative (LDS atomics), then issues one global atomic per
 // distinct representative.
 constexpr int ROOT_TB = 256, ROOT_SLOTS = 512;
-__global__ __launch_bounds__(ROOT_TB) void dc_root(DC c, int b, int j, int64_t nl) {
-    __shared__ int32_t skey[ROOT_SLOTS], smax[ROOT_SLOTS], ssum[ROOT_SLOTS], smin[ROOT_SLOTS];
+template <int TB, int SLOTS>
+__global__ __launch_bounds__(TB) void dc_root(DC c, int b, int j, int64_t nl) {
+    __shared__ int32_t skey[SLOTS], smax[SLOTS], ssum[SLOTS], smin[SLOTS];
     const int t = threadIdx.x;
-    for (int64_t base = (int64_t)blockIdx.x * ROOT_TB; base < nl; base += (int64_t)gridDim.x * ROOT_TB) {
-        for (int k = t; k < ROOT_SLOTS; k += ROOT_TB) {
+    for (int64_t base = (int64_t)blockIdx.x * TB; base < nl; base += (int64_t)gridDim.x * TB) {
+        for (int k = t; k < SLOTS; k += TB) {
             skey[k] = -1;
             smax[k] = -1;
             ssum[k] = 0;
@@ -280,18 +281,18 @@ __global__ __launch_bounds__(ROOT_TB) void dc_root(DC c, int b, int j, int64_t n
             c.hooked[r] = rep;  // dc_link reads the representative back instead of a second find
             const int32_t sz = x < 0 ? 0 : (x < c.n ? 1 : c.esize[x - c.n]);
             const int32_t mi = x < 0 ? NONE : (x < c.n ? x : c.eminid[x - c.n]);
-            uint32_t h = uf_prio(rep, 0) & (ROOT_SLOTS - 1);
-            while (true) {  // <= ROOT_TB distinct keys in 2x slots: always finds one
+            uint32_t h = uf_prio(rep, 0) & (SLOTS - 1);
+            while (true) {  // <= TB distinct keys in 2x slots: always finds one
                 int32_t k = atomicCAS(&skey[h], -1, rep);
                 if (k == -1 || k == rep) break;
-                h = (h + 1) & (ROOT_SLOTS - 1);
+                h = (h + 1) & (SLOTS - 1);
             }
             atomicMax(&smax[h], (int32_t)r);
             if (sz) atomicAdd(&ssum[h], sz);
             if (mi != NONE) atomicMin(&smin[h], mi);
         }
         __syncthreads();
-        for (int k = t; k < ROOT_SLOTS; k += ROOT_TB) {
+        for (int k = t; k < SLOTS; k += TB) {
             const int32_t rep = skey[k];
             if (rep < 0) continue;
             atomicMax(&c.lr[rep].rootedge, smax[k]);
@@ -299,6 +300,88 @@ __global__ __launch_bounds__(ROOT_TB) void dc_root(DC c, int b, int j, int64_t n
             if (smin[k] != NONE) atomicMin(&c.lr[rep].cmin, smin[k]);
         }
         __syncthreads();
+    }
+}
+
+// Several batches per workgroup with the table kept across them: a component spanning the
+// whole block (the shallow depths' giant ones) costs one set of global atomics per workgroup
+// and flush, not per batch.  The table is flushed when the next batch might overfill it.
+template <int TB, int SLOTS, int EPT>
+__global__ __launch_bounds__(TB) void dc_root_multi(DC c, int b, int j, int64_t nl) {
+    __shared__ int32_t skey[SLOTS], smax[SLOTS], ssum[SLOTS], smin[SLOTS];
+    __shared__ int s_used;
+    const int t = threadIdx.x;
+    auto clear = [&]() {
+        for (int k = t; k < SLOTS; k += TB) {
+            skey[k] = -1;
+            smax[k] = -1;
+            ssum[k] = 0;
+            smin[k] = NONE;
+        }
+        if (t == 0) s_used = 0;
+    };
+    auto flush = [&]() {
+        for (int k = t; k < SLOTS; k += TB) {
+            const int32_t rep = skey[k];
+            if (rep < 0) continue;
+            atomicMax(&c.lr[rep].rootedge, smax[k]);
+            if (ssum[k]) atomicAdd(&c.lr[rep].csize, ssum[k]);
+            if (smin[k] != NONE) atomicMin(&c.lr[rep].cmin, smin[k]);
+        }
+    };
+    const int64_t per = (int64_t)TB * EPT;
+    for (int64_t base = (int64_t)blockIdx.x * per; base < nl; base += (int64_t)gridDim.x * per) {
+        clear();
+        __syncthreads();
+        for (int e = 0; e < EPT; e++) {
+            const int64_t i = base + (int64_t)e * TB + t;
+            const int64_t r = i < nl ? l_rank(i, b) : c.m;
+            if (r < c.m) {
+                const int32_t rep = uf_find(c.lr, c.lab[2 * r]);
+                const int32_t x = c.hooked[r];
+                c.hooked[r] = rep;
+                const int32_t sz = x < 0 ? 0 : (x < c.n ? 1 : c.esize[x - c.n]);
+                const int32_t mi = x < 0 ? NONE : (x < c.n ? x : c.eminid[x - c.n]);
+                uint32_t h = uf_prio(rep, 0) & (SLOTS - 1);
+                while (true) {  // the table is kept below SLOTS - TB keys before every batch
+                    const int32_t k = atomicCAS(&skey[h], -1, rep);
+                    if (k == -1) {
+                        atomicAdd(&s_used, 1);
+                        break;
+                    }
+                    if (k == rep) break;
+                    h = (h + 1) & (SLOTS - 1);
+                }
+                atomicMax(&smax[h], (int32_t)r);
+                if (sz) atomicAdd(&ssum[h], sz);
+                if (mi != NONE) atomicMin(&smin[h], mi);
+            }
+            __syncthreads();
+            if (e + 1 < EPT && s_used > SLOTS / 2 - TB) {  // the next batch could push it past 3/4
+                flush();
+                __syncthreads();
+                clear();
+                __syncthreads();
+            }
+        }
+        flush();
+        __syncthreads();
+    }
+}
+
+// the same without the LDS table: one set of global atomics per L edge (A/B)
+__global__ void dc_root_direct(DC c, int b, int j, int64_t nl) {
+    HDB_GRID_STRIDE(i, nl) {
+        const int64_t r = l_rank(i, b);
+        if (r >= c.m) continue;
+        const int32_t rep = uf_find(c.lr, c.lab[2 * r]);
+        const int32_t x = c.hooked[r];
+        c.hooked[r] = rep;
+        atomicMax(&c.lr[rep].rootedge, (int32_t)r);
+        if (x >= 0) {
+            atomicAdd(&c.lr[rep].csize, x < c.n ? 1 : c.esize[x - c.n]);
+            atomicMin(&c.lr[rep].cmin, x < c.n ? x : c.eminid[x - c.n]);
+        }
     }
 }
 
@@ -1303,7 +1386,14 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         const int gl = grid_for(nl);
         hipLaunchKernelGGL(dc_init, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
         hipLaunchKernelGGL(dc_unite, dim3(gl), dim3(256), 0, st, dc, b, nl, err);
-        hipLaunchKernelGGL(dc_root, dim3(gl), dim3(ROOT_TB), 0, st, dc, b, j, nl);
+        switch (ctx->flat_root_variant) {
+        case 1: hipLaunchKernelGGL((dc_root<1024, 4096>), dim3((unsigned)ceil_div(nl, 1024)), dim3(1024), 0, st, dc, b, j, nl); break;
+        case 2: hipLaunchKernelGGL(dc_root_direct, dim3(gl), dim3(256), 0, st, dc, b, j, nl); break;
+        case 3: hipLaunchKernelGGL((dc_root_multi<1024, 4096, 4>), dim3((unsigned)ceil_div(nl, 4096)), dim3(1024), 0, st, dc, b, j, nl); break;
+        case 4: hipLaunchKernelGGL((dc_root_multi<1024, 8192, 4>), dim3((unsigned)ceil_div(nl, 4096)), dim3(1024), 0, st, dc, b, j, nl); break;
+        case 5: hipLaunchKernelGGL((dc_root_multi<512, 4096, 4>), dim3((unsigned)ceil_div(nl, 2048)), dim3(512), 0, st, dc, b, j, nl); break;
+        default: hipLaunchKernelGGL((dc_root<ROOT_TB, ROOT_SLOTS>), dim3(gl), dim3(ROOT_TB), 0, st, dc, b, j, nl);
+        }
         hipLaunchKernelGGL(dc_link, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
     }
     const unsigned nblk = (unsigned)std::min<int64_t>(ceil_div(m, int64_t(1) << LB), 65536);

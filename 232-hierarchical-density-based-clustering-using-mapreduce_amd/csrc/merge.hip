@@ -218,23 +218,27 @@ __device__ __forceinline__ int32_t local_of(const int32_t *keys, const int32_t *
 }
 
 __global__ void local_ids_kernel(const int32_t *__restrict__ keys, const int32_t *__restrict__ pos, int64_t n,
-                                 const int32_t *__restrict__ va, const int32_t *__restrict__ vb, int64_t ne,
-                                 int32_t node, int32_t *__restrict__ f1, int32_t *__restrict__ f2,
-                                 int32_t *__restrict__ nd, int *__restrict__ err) {
+                                 const int32_t *__restrict__ va, const int32_t *__restrict__ vb,
+                                 const double *__restrict__ w, int64_t ne, int32_t node, int32_t *__restrict__ f1,
+                                 int32_t *__restrict__ f2, int32_t *__restrict__ nd, int *__restrict__ err) {
     HDB_GRID_STRIDE(e, ne) {
+        // a tree edge never relaxed keeps Java's default nearestneighborsID = 0
+        // (CreateLocalMST.java:203,242; weight still Double.MAX_VALUE)
+        const bool unset = w && e < n - 1 && w[e] == JMAX;
         if (keys) {
-            f1[e] = local_of(keys, pos, n, va[e], err);
+            f1[e] = unset ? 0 : local_of(keys, pos, n, va[e], err);
             f2[e] = local_of(keys, pos, n, vb[e], err);
         } else {
-            f1[e] = va[e];
+            f1[e] = unset ? 0 : va[e];
             f2[e] = vb[e];
         }
         if (nd) nd[e] = node;
     }
 }
 
-void local_mst_ids_device(hdb_ctx *ctx, const int32_t *ids, int64_t n, const int32_t *va, const int32_t *vb, int64_t ne,
-                          int32_t node, int32_t *fake1, int32_t *fake2, int32_t *node_out) {
+void local_mst_ids_device(hdb_ctx *ctx, const int32_t *ids, int64_t n, const int32_t *va, const int32_t *vb,
+                          const double *w, int64_t ne, int32_t node, int32_t *fake1, int32_t *fake2,
+                          int32_t *node_out) {
     if (ne <= 0) return;
     hipStream_t st = ctx->stream;
     const int g = (int)std::min<int64_t>(ceil_div(ne, 256), 8192);
@@ -266,7 +270,7 @@ void local_mst_ids_device(hdb_ctx *ctx, const int32_t *ids, int64_t n, const int
         hipLaunchKernelGGL(local_ids_dup_kernel, dim3((int)std::min<int64_t>(ceil_div(n, 256), 8192)), dim3(256), 0, st,
                            keys, n, err);
     }
-    hipLaunchKernelGGL(local_ids_kernel, dim3(g), dim3(256), 0, st, keys, pos, n, va, vb, ne, node, fake1, fake2,
+    hipLaunchKernelGGL(local_ids_kernel, dim3(g), dim3(256), 0, st, keys, pos, n, va, vb, w, ne, node, fake1, fake2,
                        node_out, err);
     int h = 0;
     HIP_CHECK(hipMemcpyAsync(&h, err, sizeof(int), hipMemcpyDeviceToHost, st));

@@ -175,11 +175,11 @@ class HDBSCANStar:
         va, vb, w = g.getVerticeA(), g.getVericeB(), g.getEges()
         n = A.Arr(dataSet, np.float64).obj.shape[0]
         ids = A.Arr(indices, np.int32) if indices is not None else None
-        a, b = A.Arr(va, np.int32), A.Arr(vb, np.int32)
+        a, b, ww = A.Arr(va, np.int32), A.Arr(vb, np.int32), A.Arr(w, np.float64)
         ne = a.obj.shape[0]
         f1, f2, nd = (A.new_like(a, (ne,), np.int32) for _ in range(3))
         c = _ctx(a, self.ctx)
-        A.check(A.lib().hdb_local_mst_ids(c.h, ids.p if ids else None, n, a.p, b.p, ne, int(node), A.ptr(f1),
+        A.check(A.lib().hdb_local_mst_ids(c.h, ids.p if ids else None, n, a.p, b.p, ww.p, ne, int(node), A.ptr(f1),
                                           A.ptr(f2), A.ptr(nd)), "hdb_local_mst_ids")
         return va, vb, w, f1, f2, nd
 

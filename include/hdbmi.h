@@ -237,10 +237,14 @@ int hdb_merge_edges(hdb_comm *comm, const int32_t *va, const int32_t *vb, const 
  * hdb_exact_mst output), fake1[e] / fake2[e] = the local index of va[e] / vb[e] in the
  * partition's `indices` (ids, n; NULL = identity), node_out[e] = node (nullable).  On
  * hdb_prim_mst's output this is exactly nearestneighborsID / otherVertexIndicesID, so
- * hdb_format_mst_records reproduces the reference's local-MST text.  Errors: HDB_EINVAL on
- * duplicate ids or an edge vertex outside the partition.  Synchronises. */
-int hdb_local_mst_ids(hdb_ctx *ctx, const int32_t *ids, int64_t n, const int32_t *va, const int32_t *vb, int64_t ne,
-                      int32_t node, int32_t *fake1, int32_t *fake2, int32_t *node_out);
+ * hdb_format_mst_records reproduces the reference's local-MST text.  w (nullable) = the
+ * edge weights of hdb_prim_mst's layout (n - 1 tree edges first): a tree edge whose weight is
+ * still Double.MAX_VALUE was never relaxed (every MRD NaN or >= MAX_VALUE), and the
+ * reference keeps its Java default nearestneighborsID = 0 (CreateLocalMST.java:203,242) --
+ * fake1 = 0 there, whatever va holds.  Errors: HDB_EINVAL on duplicate ids or an edge vertex
+ * outside the partition.  Synchronises. */
+int hdb_local_mst_ids(hdb_ctx *ctx, const int32_t *ids, int64_t n, const int32_t *va, const int32_t *vb,
+                      const double *w, int64_t ne, int32_t node, int32_t *fake1, int32_t *fake2, int32_t *node_out);
 
 /* ------------------------------------------------ global flat labels (§8(f) #1)
  * The step the reference never completes (Main.java:351-408): HDBSCAN* hierarchy over the

@@ -173,6 +173,28 @@ def test_dataset_to_local_mst_text_on_device(pkg, oracle):
 
 
 @pytest.mark.gpu
+def test_create_local_mst_unrelaxed_vertices(pkg, oracle):
+    """rows at infinity / NaN: their mutual-reachability distances are inf or NaN, never below
+    Double.MAX_VALUE, so Prim never relaxes them and the reference keeps the Java defaults
+    (nearestMRDNeighbors = 0, nearestneighborsID = 0, weight MAX_VALUE; CreateLocalMST.java:
+    203,242) -- the record fields must say 0 there, not the local index of global id 0"""
+    from conftest import load_iris
+    X = load_iris()[:40].copy()
+    X[7] = np.inf
+    X[23, 1] = np.nan
+    n = X.shape[0]
+    # global id 0 absent, and present at the last local position
+    for ids in (np.arange(100, 100 + n, dtype=np.int32), np.r_[np.arange(5, 5 + n - 1), 0].astype(np.int32)):
+        star = pkg.HDBSCANStar()
+        core = oracle.core_distances(X, 4, semantics=oracle.EXCL_SELF)
+        got = star.constructLocalMST(X, ids, core, True, None, 3)
+        ref = oracle.create_local_mst(X, core, ids, 3)
+        assert np.any(ref[2][: n - 1] == np.finfo(np.float64).max)  # some vertex was never relaxed
+        for g, r in zip(got, ref):
+            assert np.array_equal(np.asarray(g), r)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("which", ["iris", "skin"])
 def test_create_local_mst_text_byte_exact(pkg, oracle, which):
     """CreateLocalMST end to end on the device: EXCL_SELF cores (CreateLocalMST.java:138-185),
@@ -196,11 +218,11 @@ def test_create_local_mst_text_byte_exact(pkg, oracle, which):
     f1, f2, nd = (np.zeros(va.shape[0], np.int32) for _ in range(3))
     ctx = pkg.Context.get(0)
     A = pkg._capi
-    A.check(A.lib().hdb_local_mst_ids(ctx.h, A.ptr(ids), n, A.ptr(va), A.ptr(vb), va.shape[0], 5, A.ptr(f1),
+    A.check(A.lib().hdb_local_mst_ids(ctx.h, A.ptr(ids), n, A.ptr(va), A.ptr(vb), None, va.shape[0], 5, A.ptr(f1),
                                       A.ptr(f2), A.ptr(nd)), "local ids")
     assert np.array_equal(ids[f1], va) and np.array_equal(ids[f2], vb) and np.all(nd == 5)
     bad = va.copy()
     bad[0] = 10 * n + 1
     with pytest.raises(pkg.HdbError):
-        A.check(A.lib().hdb_local_mst_ids(ctx.h, A.ptr(ids), n, A.ptr(bad), A.ptr(vb), va.shape[0], 5, A.ptr(f1),
-                                          A.ptr(f2), A.ptr(nd)), "local ids")
+        A.check(A.lib().hdb_local_mst_ids(ctx.h, A.ptr(ids), n, A.ptr(bad), A.ptr(vb), None, va.shape[0], 5,
+                                          A.ptr(f1), A.ptr(f2), A.ptr(nd)), "local ids")
