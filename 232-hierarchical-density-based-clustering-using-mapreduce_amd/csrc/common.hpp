@@ -78,10 +78,12 @@ struct hdb_ctx {
     int trav_pop_test = 0;         // bit 0: Boruvka re-tests a popped node, bit 1: K1t a popped leaf
     bool prim_coop = true;         // cooperative single-launch Prim for 4096 < n <= 65536
     bool prim_coop_plain = true;   // launch it as a plain kernel first (cooperative launches serialise)
+    bool prim_coop_xcd = true;     // plain attempt: working blocks on one XCD exchange through its L2 (checked at run time)
     int prim_coop_plain_spin_log2 = 20;  // plain attempt: polls per exchange before it reports non-co-residency
     int prim_coop_slots = 4;  // cooperative Prim exchange, rows in registers (d <= 16): 1 release/acquire slots, 2 granules,
                               // 3 drained sc1 slots, 4 DPP folds + key granules (default), 5 key+row granule sweep
     bool merge_runs = false;   // merge sort: radix-sort only what follows a non-decreasing prefix, then merge (slower as built: sync + binary searches)
+    int flat_link_variant = 1;  // K6 dc_link A/B: 0 direct guarded atomics, 1 LDS-combined multi-batch
     int flat_root_variant = 3;  // K6 dc_root A/B: 0 LDS table (256 threads), 1 (1024), 2 direct atomics, 3-5 multi-batch
     int flat_block_log = 10;   // K6: deep depths per workgroup in LDS (2^x ranks, 8-10; 0: the sequential dc_local)
     bool count_evals = false;  // K1t counts evaluated pairs (diagnostic; costs one sync)

@@ -165,6 +165,8 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         // per-kernel HIP-event timing from birth (contexts created on worker threads, bench.py)
         if (const char *e = getenv("HDB_KERNEL_TIMING")) c->timing = atoi(e) != 0;
         if (const char *e = getenv("HDB_FLAT_BLOCK_LOG")) c->flat_block_log = atoi(e);  // A/B knob
+        if (const char *e = getenv("HDB_PRIM_XCD")) c->prim_coop_xcd = atoi(e) != 0;       // A/B knob
+        if (const char *e = getenv("HDB_FLAT_LINK")) c->flat_link_variant = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_FLAT_ROOT")) c->flat_root_variant = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_MERGE_RUNS")) c->merge_runs = atoi(e) != 0;      // A/B knob
         *out = c;
@@ -283,6 +285,10 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
     }
     if (k == "prim_coop_plain") {
         ctx->prim_coop_plain = value != 0;
+        return HDB_OK;
+    }
+    if (k == "prim_coop_xcd") {
+        ctx->prim_coop_xcd = value != 0;
         return HDB_OK;
     }
     if (k == "prim_coop_plain_spin_log2") {

@@ -412,6 +412,80 @@ __global__ void dc_link(DC c, int b, int j, int64_t nl) {
     }
 }
 
+// dc_link with the parent minima combined per workgroup first (LDS table keyed by the root
+// edge R, several batches per workgroup): the U edges around a giant L component all target
+// its root edge, and their global atomicMins on one address serialise.
+template <int TB, int SLOTS, int EPT>
+__global__ __launch_bounds__(TB) void dc_link_multi(DC c, int b, int j, int64_t nl) {
+    __shared__ int32_t skey[SLOTS], smin[SLOTS];
+    __shared__ int s_used;
+    const int t = threadIdx.x;
+    auto clear = [&]() {
+        for (int k = t; k < SLOTS; k += TB) {
+            skey[k] = -1;
+            smin[k] = INT32_MAX;
+        }
+        if (t == 0) s_used = 0;
+    };
+    auto flush = [&]() {
+        for (int k = t; k < SLOTS; k += TB) {
+            const int32_t R = skey[k];
+            if (R < 0) continue;
+            if (((volatile int32_t *)c.parent)[R] > smin[k]) atomicMin(&c.parent[R], smin[k]);
+        }
+    };
+    const int64_t per = (int64_t)TB * EPT;
+    for (int64_t base = (int64_t)blockIdx.x * per; base < nl; base += (int64_t)gridDim.x * per) {
+        clear();
+        __syncthreads();
+        for (int e = 0; e < EPT; e++) {
+            const int64_t i = base + (int64_t)e * TB + t;
+            const int64_t r = i < nl ? l_rank(i, b) : c.m;
+            if (r < c.m) {
+                {  // L edge: a component root records |C(e)| and its smallest id (rep from dc_root)
+                    const int32_t rep = c.hooked[r];
+                    const LRec q = c.lr[rep];
+                    if (q.rootedge == (int32_t)r) {
+                        c.esize[r] = q.csize + (rep < c.n ? 1 : c.esize[rep - c.n]);
+                        c.eminid[r] = min(q.cmin, rep < c.n ? rep : c.eminid[rep - c.n]);
+                    }
+                }
+                const int64_t u = r | (int64_t(1) << b);
+                if (u < c.m) {
+#pragma unroll
+                    for (int s = 0; s < 2; s++) {
+                        const int32_t x = c.lab[2 * u + s];
+                        if (c.stamp[x] == 2 * j) {
+                            const int32_t R = c.lr[uf_find(c.lr, x)].rootedge;
+                            uint32_t h = uf_prio(R, 0) & (SLOTS - 1);
+                            while (true) {  // <= SLOTS / 2 keys before every batch's 2 TB inserts
+                                const int32_t k = atomicCAS(&skey[h], -1, R);
+                                if (k == -1) {
+                                    atomicAdd(&s_used, 1);
+                                    break;
+                                }
+                                if (k == R) break;
+                                h = (h + 1) & (SLOTS - 1);
+                            }
+                            atomicMin(&smin[h], (int32_t)u);
+                            c.lab[2 * u + s] = (int32_t)(c.n + R);
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            if (e + 1 < EPT && s_used > SLOTS / 2 - 2 * TB) {
+                flush();
+                __syncthreads();
+                clear();
+                __syncthreads();
+            }
+        }
+        flush();
+        __syncthreads();
+    }
+}
+
 // Deep depths in one launch, in parallel: a workgroup takes a block of 2^LB consecutive ranks
 // whose labels name the components of F_{<lo} and runs the same rank divide and conquer on
 // LDS (labels hashed to local ids, contracted labels = HS + local root-edge rank, an LDS
@@ -1394,7 +1468,11 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         case 5: hipLaunchKernelGGL((dc_root_multi<512, 4096, 4>), dim3((unsigned)ceil_div(nl, 2048)), dim3(512), 0, st, dc, b, j, nl); break;
         default: hipLaunchKernelGGL((dc_root<ROOT_TB, ROOT_SLOTS>), dim3(gl), dim3(ROOT_TB), 0, st, dc, b, j, nl);
         }
-        hipLaunchKernelGGL(dc_link, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
+        if (ctx->flat_link_variant == 1)
+            hipLaunchKernelGGL((dc_link_multi<1024, 8192, 2>), dim3((unsigned)ceil_div(nl, 2048)), dim3(1024), 0, st, dc,
+                               b, j, nl);
+        else
+            hipLaunchKernelGGL(dc_link, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
     }
     const unsigned nblk = (unsigned)std::min<int64_t>(ceil_div(m, int64_t(1) << LB), 65536);
     switch (ctx->flat_block_log) {

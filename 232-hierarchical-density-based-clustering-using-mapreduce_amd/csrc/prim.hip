@@ -883,11 +883,18 @@ static bool launch_coop3(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
 // key granules {value lo, value hi, index} + 2 (DM + 3) row granules, one sc1 store per lane),
 // sweeps the nwg x 3 key granules flat until every tag is this step, picks the winner workgroup
 // and reads its row granules straight into the LDS row; ONE barrier.  No fences, no counters.
+// Same-XCD exchange (spread = 8): the grid is 8x the workgroups and only blocks b % 8 == 0
+// work -- blocks b and b + 8 are dealt to one XCD.  They check that at run time (XCC_ID): when
+// every working block reports the same XCC, the granules are published with plain stores (the
+// line stays in that XCD's L2, which every CU's sc1 poll reads) instead of sc1 stores (which
+// drop the line from L2, so every poll crossed the fabric).  Any other placement keeps the sc1
+// protocol: placement changes only speed.
 template <int BS, int DM, bool FULL>
 __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int self_edges, int32_t *__restrict__ va,
                                                         int32_t *__restrict__ vb, double *__restrict__ w,
                                                         gu64 *__restrict__ gkey, gu64 *__restrict__ grow, int *err,
-                                                        unsigned spin_limit) {
+                                                        unsigned spin_limit, int spread, int *__restrict__ xcc) {
+    if (blockIdx.x % spread) return;  // an idle block of a spread grid
     constexpr int NW = BS / 64;
     constexpr int ND = DM + 3;  // x, core, eB, nnB
     __shared__ double s_cand[NW][ND + 1];
@@ -895,10 +902,50 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
     constexpr int G = 3 + 2 * ND;  // FULL: one slot of key + row granules per workgroup
     __shared__ unsigned s_key[FULL ? G * 64 : 3 * 64];
     __shared__ double s_row[ND];
-    __shared__ int s_cur;
-    const int nwg = (int)gridDim.x;
+    __shared__ int s_cur, s_local;
+    const int nwg = (int)gridDim.x / spread;
+    const int bid = (int)blockIdx.x / spread;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int i = (int)blockIdx.x * BS + tid;
+    const int i = bid * BS + tid;
+    if (tid == 0) s_local = 0;
+    if (spread > 1 && wid == 0) {  // every working block on one XCC?
+        if (lane == 0) {
+            unsigned x;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+            __hip_atomic_store(xcc + bid, (int)(x & 15u) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bool same = true;
+        int first = 0;
+        for (unsigned spins = 0;;) {
+            bool ok = true;
+            int mn = 1 << 30, mx = -1;
+            for (int j = lane; j < nwg; j += 64) {
+                const int v = __hip_atomic_load(xcc + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok &= v != 0;
+                mn = min(mn, v);
+                mx = max(mx, v);
+            }
+            if (__all(ok)) {
+                for (int o = 32; o >= 1; o >>= 1) {
+                    mn = min(mn, __shfl_xor(mn, o));
+                    mx = max(mx, __shfl_xor(mx, o));
+                }
+                same = mn == mx;
+                first = mn;
+                break;
+            }
+            if (++spins > spin_limit) {  // not co-resident: the retry takes over
+                if (lane == 0) atomicExch(err, 1);
+                first = -1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (lane == 0) s_local = first < 0 ? -1 : (same && first > 0);
+    }
+    __syncthreads();
+    if (s_local < 0) return;
+    const bool local = s_local != 0;
     double xi[DM], ci = 0, ebi = 0, nni = 0;
 #pragma unroll
     for (int c = 0; c < DM; c++) xi[c] = (i < n && c < in.d) ? in.X[(int64_t)i * in.d + c] : 0.0;
@@ -963,16 +1010,19 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
             else if (lane == 2) val = (unsigned)gidx;
             else val = lane < 3 + 2 * ND ? cw[lane - 3] : 0u;
             const unsigned long long gv = ((unsigned long long)tag << 32) | val;
+            gu64 *dst = nullptr;
             if (FULL) {
-                if (lane < G)
-                    __hip_atomic_store(gkey + ((size_t)buf * nwg + blockIdx.x) * G + lane, gv, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+                if (lane < G) dst = gkey + ((size_t)buf * nwg + bid) * G + lane;
             } else if (lane < 3)
-                __hip_atomic_store(gkey + ((size_t)buf * nwg + blockIdx.x) * 3 + lane, gv, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+                dst = gkey + ((size_t)buf * nwg + bid) * 3 + lane;
             else if (lane < 3 + 2 * ND)
-                __hip_atomic_store(grow + ((size_t)buf * nwg + blockIdx.x) * (2 * ND) + (lane - 3), gv, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+                dst = grow + ((size_t)buf * nwg + bid) * (2 * ND) + (lane - 3);
+            if (dst) {
+                if (local)  // plain store: the line stays in the XCD's L2 the other blocks poll
+                    __hip_atomic_store(dst, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else
+                    __hip_atomic_store(dst, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             COOP_T(2);
             // sweep every workgroup's key granules
             constexpr int KS = FULL ? G : 3;  // granules per workgroup in the sweep
@@ -1075,11 +1125,12 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
     constexpr int ND = DM + 3;
     const size_t kbytes = (8 * (size_t)(FULL ? 3 + 2 * ND : 3) * 2 * nwg + 255) & ~size_t(255);
     const size_t rbytes = (8 * (size_t)2 * ND * 2 * nwg + 255) & ~size_t(255);
-    char *base = (char *)arena(ctx, A_WORK3, kbytes + rbytes + 256);
+    char *base = (char *)arena(ctx, A_WORK3, kbytes + rbytes + 512);
     gu64 *gkey = (gu64 *)base;
     gu64 *grow = (gu64 *)(base + kbytes);
     int *err = (int *)(base + kbytes + rbytes);
-    HIP_CHECK(hipMemsetAsync(base, 0, kbytes + rbytes + 256, ctx->stream));  // tags 0: no step yet
+    int *xcc = err + 64;  // the working blocks' XCC ids (spread launch)
+    HIP_CHECK(hipMemsetAsync(base, 0, kbytes + rbytes + 512, ctx->stream));  // tags 0: no step yet
     PrimIn L = in;
     L.X = in.X + o * in.d;
     L.core = in.core + o;
@@ -1092,7 +1143,10 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
     int32_t *pva = va + eo, *pvb = vb + eo;
     double *pw = w + eo;
     unsigned spin = 1u << 24;
-    void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &gkey, &grow, &err, &spin};
+    int spread1 = 1;
+    void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &gkey, &grow, &err, &spin, &spread1, &xcc};
+    // same-XCD exchange for the plain attempt when its blocks fit one XCD twice over
+    const int spread = (ctx->prim_coop_xcd && nwg <= 16) ? 8 : 1;
     // A plain launch first: ROCm serialises cooperative launches device-wide, so the concurrent
     // local models of one level (driver model pool) would queue behind each other.  The grid
     // (<= 64 workgroups) is far below the device's capacity, and every inter-workgroup wait has
@@ -1104,12 +1158,12 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
     const unsigned plain_spin = 1u << ctx->prim_coop_plain_spin_log2;
     int h_err = 0;
     for (int attempt = ctx->prim_coop_plain ? 0 : 1; attempt < 2; attempt++) {
-        if (attempt == 1 && h_err) HIP_CHECK(hipMemsetAsync(base, 0, kbytes + rbytes + 256, ctx->stream));
+        if (attempt == 1 && h_err) HIP_CHECK(hipMemsetAsync(base, 0, kbytes + rbytes + 512, ctx->stream));
         {
             KernelTimer t(ctx, "prim_coop");
             if (attempt == 0)
-                hipLaunchKernelGGL((prim_coop4_kernel<BS, DM, FULL>), dim3(nwg), dim3(BS), 0, ctx->stream, L, nn,
-                                   self_edges, pva, pvb, pw, gkey, grow, err, plain_spin);
+                hipLaunchKernelGGL((prim_coop4_kernel<BS, DM, FULL>), dim3(nwg * spread), dim3(BS), 0, ctx->stream, L, nn,
+                                   self_edges, pva, pvb, pw, gkey, grow, err, plain_spin, spread, xcc);
             else
                 HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_coop4_kernel<BS, DM, FULL>, dim3(nwg), dim3(BS),
                                                      args, 0, ctx->stream));

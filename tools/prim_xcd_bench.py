@@ -1,0 +1,48 @@
+"""Cooperative Prim step cost with and without the same-XCD exchange (prim_coop_xcd), plain
+reference Prim and bubble Prim, and a check that both give identical edges.
+usage: python tools/prim_xcd_bench.py [n] [d]"""
+import importlib
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+pkg = importlib.import_module("232-hierarchical-density-based-clustering-using-mapreduce_amd")
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+d = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+rng = np.random.default_rng(0)
+X = torch.from_numpy(rng.normal(size=(n, d)) * 10).cuda()
+core = torch.from_numpy(np.abs(rng.normal(0.5, 0.1, n))).cuda()
+eB = torch.from_numpy(np.abs(rng.normal(0.3, 0.1, n))).cuda()
+nnB = torch.from_numpy(np.abs(rng.normal(0.2, 0.05, n))).cuda()
+nB = torch.from_numpy(rng.integers(1, 9, n).astype(np.int32)).cuda()
+ids = torch.arange(n, dtype=torch.int32).cuda()
+ctx = pkg.Context.get(0)
+ctx.use_torch_stream()
+star, model = pkg.HDBSCANStar(ctx), pkg.HdbscanDataBubbles(ctx)
+out = {}
+for rep in range(2):
+    for xcd in (0, 1):
+        ctx.set_option("prim_coop_xcd", xcd)
+        for name, f in (("prim", lambda: star.constructMST(X, core, True, None, ids)),
+                        ("bubble_prim", lambda: model.constructMSTBubbles(X, nB, eB, nnB, ids, core, True))):
+            g = f()
+            torch.cuda.synchronize()
+            r0 = ctx.get_stat("prim_coop_plain_retries")
+            t = time.perf_counter()
+            for _ in range(3):
+                g = f()
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t) / 3
+            e = tuple(np.asarray(x.cpu() if hasattr(x, "cpu") else x) for x in (g.getVerticeA(), g.getVericeB(), g.getEges()))
+            key = name
+            if key in out:
+                assert all(np.array_equal(a, b) for a, b in zip(out[key], e)), f"{name}: edges differ with xcd={xcd}"
+            out[key] = e
+            print(f"xcd={xcd} {name:12s} n={n} d={d}: {dt * 1e3:8.2f} ms  ({dt / n * 1e6:.2f} us/step)  "
+                  f"retries {ctx.get_stat('prim_coop_plain_retries') - r0}", flush=True)
+ctx.set_option("prim_coop_xcd", 1)
+print("edges identical across xcd settings")
