@@ -166,6 +166,7 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         if (const char *e = getenv("HDB_KERNEL_TIMING")) c->timing = atoi(e) != 0;
         if (const char *e = getenv("HDB_FLAT_BLOCK_LOG")) c->flat_block_log = atoi(e);  // A/B knob
         if (const char *e = getenv("HDB_PRIM_XCD")) c->prim_coop_xcd = atoi(e) != 0;       // A/B knob
+        if (const char *e = getenv("HDB_PRIM_XCD_MAX_WG")) c->prim_coop_xcd_max_wg = atoi(e);  // A/B knob
         if (const char *e = getenv("HDB_FLAT_LINK")) c->flat_link_variant = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_FLAT_ROOT")) c->flat_root_variant = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_MERGE_RUNS")) c->merge_runs = atoi(e) != 0;      // A/B knob

@@ -1125,7 +1125,6 @@ __global__ __launch_bounds__(64) void fo_walk(FoscArr a, int d, const int *__res
     if (*bad & (FE_CYCLE | FE_ROOTS)) return;  // malformed input: reported by the caller
     if (d > *a.maxld) return;
     __shared__ double s_st[FO_CHUNK], s_lv[FO_CHUNK], s_out[FO_CHUNK];
-    __shared__ int32_t s_sel[FO_CHUNK];
     const int lane = threadIdx.x;
     const int32_t K = *a.Kp, NL = *a.lcount;
     for (int32_t j = blockIdx.x; j < NL; j += gridDim.x) {
@@ -1149,7 +1148,6 @@ __global__ __launch_bounds__(64) void fo_walk(FoscArr a, int d, const int *__res
             if (hi == tlen - 1) {  // the path's bottom: a leaf, its own stability
                 acc = s_st[0];
                 s_out[0] = acc;
-                s_sel[0] = 1;
                 i = 1;
             }
             while (i < cnt) {
@@ -1168,8 +1166,7 @@ __global__ __launch_bounds__(64) void fo_walk(FoscArr a, int d, const int *__res
                         const double prop = acc + lv8[u];  // binary: a + b == b + a
                         const bool sq = st8[u] >= prop;    // ties keep the parent
                         acc = sq ? st8[u] : prop;
-                        s_out[q + u] = acc;
-                        s_sel[q + u] = sq;
+                        s_out[q + u] = acc;  // self-selected <=> out == st (st >= prop keeps st)
                     }
                 }
                 for (; q < e; q++) {
@@ -1177,7 +1174,6 @@ __global__ __launch_bounds__(64) void fo_walk(FoscArr a, int d, const int *__res
                     const bool sq = st1 >= prop;
                     acc = sq ? st1 : prop;
                     s_out[q] = acc;
-                    s_sel[q] = sq;
                 }
                 if (e < cnt) {  // a multi-way node: (sum before the heavy child) + heavy + the rest
                     const int32_t cm = __builtin_amdgcn_readlane(c, e);
@@ -1193,7 +1189,6 @@ __global__ __launch_bounds__(64) void fo_walk(FoscArr a, int d, const int *__res
                     const bool sm = stm >= prop;
                     acc = sm ? stm : prop;
                     s_out[e] = acc;
-                    s_sel[e] = sm;
                     i = e + 1;
                 } else {
                     i = e;
@@ -1201,8 +1196,10 @@ __global__ __launch_bounds__(64) void fo_walk(FoscArr a, int d, const int *__res
             }
             __syncthreads();
             if (lane < cnt) {
-                a.cp[c] = s_out[lane];
-                a.ssel[c] = s_sel[lane];
+                const double o = s_out[lane];
+                a.cp[c] = o;
+                // st >= prop kept st; otherwise out = prop != st (or NaN); a leaf always keeps its own
+                a.ssel[c] = (o == s_st[lane]) || (lane == 0 && hi == tlen - 1);
             }
             __syncthreads();
         }

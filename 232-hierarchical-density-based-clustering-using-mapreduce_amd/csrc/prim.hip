@@ -17,6 +17,8 @@
 //                       captured hipGraph chunk.
 // Euclidean pairs use a squared filter: s > fl(b*b)*(1+2^-50) proves sqrt(s) >= b, so
 // the exact sqrt + mrd path runs only for pairs that can improve best[nb].
+#include <atomic>
+
 #include "internal.hpp"
 
 namespace hdb {
@@ -883,8 +885,9 @@ static bool launch_coop3(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
 // key granules {value lo, value hi, index} + 2 (DM + 3) row granules, one sc1 store per lane),
 // sweeps the nwg x 3 key granules flat until every tag is this step, picks the winner workgroup
 // and reads its row granules straight into the LDS row; ONE barrier.  No fences, no counters.
-// Same-XCD exchange (spread = 8): the grid is 8x the workgroups and only blocks b % 8 == 0
-// work -- blocks b and b + 8 are dealt to one XCD.  They check that at run time (XCC_ID): when
+// Same-XCD exchange (spread = 8): the grid is 8x the workgroups and only blocks b % 8 == res
+// work -- blocks b and b + 8 are dealt to one XCD (res rotates per launch, so concurrent Prims
+// of the model pool tend to land on different XCDs).  They check that at run time (XCC_ID): when
 // every working block reports the same XCC, the granules are published with plain stores (the
 // line stays in that XCD's L2, which every CU's sc1 poll reads) instead of sc1 stores (which
 // drop the line from L2, so every poll crossed the fabric).  Any other placement keeps the sc1
@@ -893,8 +896,9 @@ template <int BS, int DM, bool FULL>
 __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int self_edges, int32_t *__restrict__ va,
                                                         int32_t *__restrict__ vb, double *__restrict__ w,
                                                         gu64 *__restrict__ gkey, gu64 *__restrict__ grow, int *err,
-                                                        unsigned spin_limit, int spread, int *__restrict__ xcc) {
-    if (blockIdx.x % spread) return;  // an idle block of a spread grid
+                                                        unsigned spin_limit, int spread, int *__restrict__ xcc,
+                                                        int res) {
+    if ((int)(blockIdx.x % spread) != res) return;  // an idle block of a spread grid
     constexpr int NW = BS / 64;
     constexpr int ND = DM + 3;  // x, core, eB, nnB
     __shared__ double s_cand[NW][ND + 1];
@@ -1143,10 +1147,12 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
     int32_t *pva = va + eo, *pvb = vb + eo;
     double *pw = w + eo;
     unsigned spin = 1u << 24;
-    int spread1 = 1;
-    void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &gkey, &grow, &err, &spin, &spread1, &xcc};
-    // same-XCD exchange for the plain attempt when its blocks fit one XCD twice over
-    const int spread = (ctx->prim_coop_xcd && nwg <= 16) ? 8 : 1;
+    int spread1 = 1, res0 = 0;
+    void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &gkey, &grow, &err, &spin, &spread1, &xcc, &res0};
+    // same-XCD exchange for the plain attempt when its blocks fit one XCD (32 CUs)
+    const int spread = (ctx->prim_coop_xcd && nwg <= ctx->prim_coop_xcd_max_wg && nwg <= 32 * per_cu) ? 8 : 1;
+    static std::atomic<int> launches{0};
+    const int res = spread > 1 ? (launches.fetch_add(1) & 7) : 0;
     // A plain launch first: ROCm serialises cooperative launches device-wide, so the concurrent
     // local models of one level (driver model pool) would queue behind each other.  The grid
     // (<= 64 workgroups) is far below the device's capacity, and every inter-workgroup wait has
@@ -1163,7 +1169,7 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
             KernelTimer t(ctx, "prim_coop");
             if (attempt == 0)
                 hipLaunchKernelGGL((prim_coop4_kernel<BS, DM, FULL>), dim3(nwg * spread), dim3(BS), 0, ctx->stream, L, nn,
-                                   self_edges, pva, pvb, pw, gkey, grow, err, plain_spin, spread, xcc);
+                                   self_edges, pva, pvb, pw, gkey, grow, err, plain_spin, spread, xcc, res);
             else
                 HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_coop4_kernel<BS, DM, FULL>, dim3(nwg), dim3(BS),
                                                      args, 0, ctx->stream));
