@@ -194,23 +194,150 @@ __global__ __launch_bounds__(256) void bubble_knn_kernel(const double *__restric
     }
 }
 
+// The candidate range split in S chunks (grid.y): a 16k-bubble model as one thread per bubble
+// is 256 waves -- one per CU, latency bound.  The sequential kernel's log is an insertion log
+// per position (lg is not shifted: the stale indexBubbles emulation), so the chunks cannot be
+// merged as lists.  Instead each chunk scans its candidates with a chunk-local buffer and
+// records every local insertion (q, dist) in q order.  Every insertion of the sequential scan
+// is among them: the chunk's buffer holds a subset of the sequential buffer's candidates, so
+// its K-th value is never smaller.  Replaying the recorded events of chunks 0..S-1 in q order
+// with the sequential rule then reproduces the buffer and the log exactly (a recorded event
+// the sequential scan would not insert fails the same test in the replay; an unrecorded one
+// would not have changed the state).  A chunk with more insertions than it can record sets a flag and
+// the sequential kernel runs instead (BK_EV events per chunk).
+constexpr int BK_EV = 64;
+template <int KC>
+__global__ __launch_bounds__(256) void bubble_knn_part_kernel(const double *__restrict__ rep,
+                                                              const double *__restrict__ eB,
+                                                              const double *__restrict__ nnB, int64_t b, int d,
+                                                              int metric, int K, int S, double *__restrict__ evd,
+                                                              int32_t *__restrict__ evq, int32_t *__restrict__ evn,
+                                                              int *__restrict__ overflow) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int s = blockIdx.y;
+    const int64_t pr = p < b ? p : 0;
+    const int64_t q0 = b * s / S, q1 = b * (s + 1) / S;
+    const int64_t eo = ((int64_t)s * b + pr) * BK_EV;
+    double buf[KC];
+#pragma unroll
+    for (int k = 0; k < KC; k++) buf[k] = JMAX;
+    int ne = 0;
+    const double ep = eB[pr], np_ = nnB[pr];
+    const double *xp = rep + pr * d;
+    for (int64_t q = q0; q < q1; q++) {  // wave-uniform loop
+        if (q == p) continue;
+        double dist = metric_distance(xp, rep + q * d, d, metric);
+        dist = distance_bubbles(dist, ep, eB[q], np_, nnB[q]);
+        if (dist < buf[K - 1 < KC ? K - 1 : KC - 1]) {
+            int pos = K;
+#pragma unroll
+            for (int k = KC - 1; k >= 0; k--)
+                if (k < K && dist < buf[k]) pos = k;
+#pragma unroll
+            for (int k = KC - 1; k > 0; k--)
+                if (k < K && k > pos) buf[k] = buf[k - 1];
+#pragma unroll
+            for (int k = 0; k < KC; k++)
+                if (k == pos) buf[k] = dist;
+            if (p < b && ne < BK_EV) {
+                evd[eo + ne] = dist;
+                evq[eo + ne] = (int32_t)q;
+            }
+            ne++;
+        }
+    }
+    if (p < b) {
+        evn[(int64_t)s * b + p] = ne < BK_EV ? ne : BK_EV;
+        if (ne > BK_EV) atomicOr(overflow, 1);
+    }
+}
+
+template <int KC>
+__global__ __launch_bounds__(256) void bubble_knn_replay_kernel(const double *__restrict__ evd,
+                                                                const int32_t *__restrict__ evq,
+                                                                const int32_t *__restrict__ evn, int64_t b, int K, int S,
+                                                                double *__restrict__ knn_out,
+                                                                int32_t *__restrict__ log_out) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= b) return;
+    double buf[KC];
+    int32_t lg[KC];
+#pragma unroll
+    for (int k = 0; k < KC; k++) {
+        buf[k] = JMAX;
+        lg[k] = -1;
+    }
+    for (int s = 0; s < S; s++) {
+        const int64_t eo = ((int64_t)s * b + p) * BK_EV;
+        const int ne = evn[(int64_t)s * b + p];
+        for (int e = 0; e < ne; e++) {  // the sequential kernel's insertion, event by event
+            const double dist = evd[eo + e];
+            if (!(dist < buf[K - 1 < KC ? K - 1 : KC - 1])) continue;
+            int pos = K;
+#pragma unroll
+            for (int k = KC - 1; k >= 0; k--)
+                if (k < K && dist < buf[k]) pos = k;
+#pragma unroll
+            for (int k = KC - 1; k > 0; k--)
+                if (k < K && k > pos) buf[k] = buf[k - 1];
+#pragma unroll
+            for (int k = 0; k < KC; k++)
+                if (k == pos) {
+                    buf[k] = dist;
+                    lg[k] = evq[eo + e];
+                }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < KC; k++)
+        if (k < K) {
+            knn_out[p * K + k] = buf[k];
+            log_out[p * K + k] = lg[k];
+        }
+}
+
+template <int KC>
+static void bubble_knn_launch(hdb_ctx *ctx, const double *rep, const double *eB, const double *nnB, int64_t b, int d,
+                              int metric, int K, double *knn_out, int32_t *log_out) {
+    // chunks: >= ~256k threads per model, >= 256 candidates per chunk
+    int64_t S = std::min<int64_t>(ceil_div(262144, std::max<int64_t>(b, 1)), std::max<int64_t>(b / 256, 1));
+    S = std::max<int64_t>(1, std::min<int64_t>(S, 64));
+    if (!ctx->bubble_knn_split) S = 1;
+    const dim3 g1((unsigned)ceil_div(b, 256));
+    if (S > 1) {
+        const size_t ev = (size_t)S * b * BK_EV;
+        char *base = (char *)arena(ctx, A_WORK2, ev * (sizeof(double) + sizeof(int32_t)) + (size_t)S * b * 4 + 1024);
+        double *evd = (double *)base;
+        int32_t *evq = (int32_t *)(base + ev * sizeof(double));
+        int32_t *evn = evq + ev;
+        int *ovf = (int *)(((uintptr_t)(evn + (size_t)S * b) + 255) & ~uintptr_t(255));
+        HIP_CHECK(hipMemsetAsync(ovf, 0, sizeof(int), ctx->stream));
+        hipLaunchKernelGGL(bubble_knn_part_kernel<KC>, dim3(g1.x, (unsigned)S), dim3(256), 0, ctx->stream, rep, eB, nnB,
+                           b, d, metric, K, (int)S, evd, evq, evn, ovf);
+        hipLaunchKernelGGL(bubble_knn_replay_kernel<KC>, g1, dim3(256), 0, ctx->stream, evd, evq, evn, b, K, (int)S,
+                           knn_out, log_out);
+        int *pin = (int *)(pinned_words(ctx) + PINNED_WORDS - 24);
+        HIP_CHECK(hipMemcpyAsync(pin, ovf, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        if (*pin == 0) return;
+        ctx->stats["bubble_knn_replay_overflows"] += 1;  // adversarial candidate order: the plain scan
+    }
+    hipLaunchKernelGGL(bubble_knn_kernel<KC>, g1, dim3(256), 0, ctx->stream, rep, eB, nnB, b, d, metric, K, knn_out,
+                       log_out);
+}
+
 void bubble_knn_device(hdb_ctx *ctx, const double *rep, const double *eB, const double *nnB, int64_t b, int d,
                        int metric, int K, double *knn_out, int32_t *log_out) {
     if (b <= 0 || K <= 0) return;
-    dim3 grid((unsigned)ceil_div(b, 256));
     KernelTimer t(ctx, "bubble_knn");
     if (K <= 3)
-        hipLaunchKernelGGL(bubble_knn_kernel<3>, grid, dim3(256), 0, ctx->stream, rep, eB, nnB, b, d, metric, K, knn_out,
-                           log_out);
+        bubble_knn_launch<3>(ctx, rep, eB, nnB, b, d, metric, K, knn_out, log_out);
     else if (K <= 7)
-        hipLaunchKernelGGL(bubble_knn_kernel<7>, grid, dim3(256), 0, ctx->stream, rep, eB, nnB, b, d, metric, K, knn_out,
-                           log_out);
+        bubble_knn_launch<7>(ctx, rep, eB, nnB, b, d, metric, K, knn_out, log_out);
     else if (K <= 15)
-        hipLaunchKernelGGL(bubble_knn_kernel<15>, grid, dim3(256), 0, ctx->stream, rep, eB, nnB, b, d, metric, K,
-                           knn_out, log_out);
+        bubble_knn_launch<15>(ctx, rep, eB, nnB, b, d, metric, K, knn_out, log_out);
     else if (K <= 31)
-        hipLaunchKernelGGL(bubble_knn_kernel<31>, grid, dim3(256), 0, ctx->stream, rep, eB, nnB, b, d, metric, K,
-                           knn_out, log_out);
+        bubble_knn_launch<31>(ctx, rep, eB, nnB, b, d, metric, K, knn_out, log_out);
     else
         HDB_THROW(HDB_EINVAL, "minPts too large (max 32)");
     HIP_CHECK(hipGetLastError());

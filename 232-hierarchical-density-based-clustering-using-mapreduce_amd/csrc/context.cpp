@@ -166,6 +166,7 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         if (const char *e = getenv("HDB_KERNEL_TIMING")) c->timing = atoi(e) != 0;
         if (const char *e = getenv("HDB_FLAT_BLOCK_LOG")) c->flat_block_log = atoi(e);  // A/B knob
         if (const char *e = getenv("HDB_PRIM_XCD")) c->prim_coop_xcd = atoi(e) != 0;       // A/B knob
+        if (const char *e = getenv("HDB_BUBBLE_SPLIT")) c->bubble_knn_split = atoi(e) != 0;  // A/B knob
         if (const char *e = getenv("HDB_PRIM_XCD_MAX_WG")) c->prim_coop_xcd_max_wg = atoi(e);  // A/B knob
         if (const char *e = getenv("HDB_FLAT_LINK")) c->flat_link_variant = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_FLAT_ROOT")) c->flat_root_variant = atoi(e);      // A/B knob
@@ -286,6 +287,10 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
     }
     if (k == "prim_coop_plain") {
         ctx->prim_coop_plain = value != 0;
+        return HDB_OK;
+    }
+    if (k == "bubble_knn_split") {
+        ctx->bubble_knn_split = value != 0;
         return HDB_OK;
     }
     if (k == "prim_coop_xcd") {

@@ -551,6 +551,31 @@ def test_prim_coop_slots_metrics_and_bubbles(pkg, oracle, d, metric, n):
     assert eq(mst.getVerticeA(), ra) and eq(mst.getVericeB(), rb) and eq(mst.getEges(), rw)
 
 
+@pytest.mark.parametrize("case", ["ties", "descending"])
+def test_bubble_core_split_scan_vs_oracle(pkg, oracle, case):
+    """K5 in candidate chunks with the exact event replay (bubbles.hip): the bubble core
+    distances -- which read the sequential scan's per-position insertion log through the stale
+    indexBubbles epilogue (HdbscanDataBubbles.java:121-143) -- equal the oracle's on 9,000
+    bubbles with massive distance ties (rounded coordinates, repeated extents), and on a 1-D
+    descending layout where every candidate is a new nearest for the far points (the chunks'
+    event buffers overflow and the sequential scan takes over)."""
+    rng = np.random.default_rng(31)
+    n = 9000
+    if case == "ties":
+        X = np.round(blobs(n, 4, 12, 77, spread=10.0), 0)
+        eB = np.round(np.abs(rng.normal(0.3, 0.1, n)), 1)
+        nnB = np.round(np.abs(rng.normal(0.2, 0.05, n)), 1)
+    else:
+        X = -np.arange(n, dtype=np.float64)[:, None] * np.ones((1, 2))
+        eB = np.full(n, 0.1)
+        nnB = np.full(n, 0.05)
+    nB = rng.integers(1, 9, n).astype(np.int32)
+    model = pkg.HdbscanDataBubbles()
+    for k in (4, 8):
+        core = model.calculateCoreDistancesBubbles(X, nB, eB, nnB, k)
+        assert eq(core, oracle.bubble_core_distances(X, nB, eB, nnB, k)), (case, k)
+
+
 # ------------------------------------------- K3g (grouped samples, box pruning) vs the scan
 @pytest.mark.parametrize("d", [2, 3, 4, 8, 16])
 def test_nearest_grouped_vs_oracle(pkg, oracle, d):
