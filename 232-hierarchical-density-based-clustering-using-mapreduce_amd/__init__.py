@@ -10,7 +10,7 @@ from ._capi import (BUBBLE_CF, BUBBLE_COMBINESTEP, CORE_EXCL_SELF, CORE_INCL_SEL
                     ArrayIndexOutOfBoundsException, Context, HdbError, IllegalStateException,
                     NullPointerException, NumberFormatException, lib)
 from .databubbles import (CombineStep, FirstStep, HdbscanDataBubbles, LocalModelReduceByKey,
-                          bubble_stats, nearest_sample, sort_edges_desc)
+                          bubble_stats, merge_sorted_runs, nearest_sample, sort_edges_desc)
 from .driver import MRHDBSCANStar
 from .formats import (MapperDataset_github, double_to_string, format_local_mst, parse_local_mst,
                       read_dataset)

@@ -104,6 +104,7 @@ def lib():
             "hdb_local_model": [vp, dp, dp, i64, i32, i32, i32, i32, ip, ip, ip, dp, ip, ip, dp, lp],
             "hdb_quicksort_edges": [ip, ip, dp, i64],
             "hdb_sort_edges_desc": [vp, ip, ip, dp, i64],
+            "hdb_merge_sorted_runs": [vp, ip, ip, dp, lp, i32, ip, ip, dp],
             "hdb_flat_labels": [vp, ip, ip, dp, i64, i64, i32, ip, lp],
             "hdb_local_mst_ids": [vp, ip, i64, ip, ip, dp, i64, i32, ip, ip, ip],
             "hdb_comm_unique_id": [vp, i32],
@@ -136,7 +137,7 @@ EXPORTED = ["hdb_ctx_create", "hdb_ctx_destroy", "hdb_ctx_set_stream", "hdb_ctx_
             "hdb_distance_rows", "hdb_core_distances", "hdb_knn", "hdb_prim_mst", "hdb_prim_mst_batched",
             "hdb_leaf_msts", "hdb_mst_boruvka", "hdb_exact_mst", "hdb_nearest_sample", "hdb_bubble_stats",
             "hdb_bubble_core_distances", "hdb_bubble_prim_mst", "hdb_local_model", "hdb_quicksort_edges",
-            "hdb_sort_edges_desc", "hdb_flat_labels", "hdb_format_double", "hdb_parse_points",
+            "hdb_merge_sorted_runs", "hdb_sort_edges_desc", "hdb_flat_labels", "hdb_format_double", "hdb_parse_points",
             "hdb_format_mst_records", "hdb_parse_mst_records", "hdb_comm_unique_id", "hdb_comm_init",
             "hdb_comm_destroy", "hdb_free", "hdb_copy", "hdb_merge_edges", "hdb_local_mst_ids"]
 

@@ -422,6 +422,27 @@ int hdb_sort_edges_desc(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64
     });
 }
 
+int hdb_merge_sorted_runs(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, const double *w, const int64_t *run_off,
+                          int32_t nruns, int32_t *oa, int32_t *ob, double *ow) {
+    return guarded(ctx, [&] {
+        if (nruns < 0 || (nruns > 0 && !run_off)) HDB_THROW(HDB_EINVAL, "bad arguments");
+        std::vector<int64_t> off(run_off, run_off + nruns + 1);
+        if (nruns == 0) off.assign(1, 0);
+        for (int r = 0; r < nruns; r++)
+            if (off[r + 1] < off[r] || off[0] != 0) HDB_THROW(HDB_EINVAL, "merge_sorted_runs: bad run offsets");
+        const int64_t ne = off.back();
+        if (ne > INT32_MAX) HDB_THROW(HDB_EINVAL, "too many edges");
+        if (ne > 0 && (!va || !vb || !w || !oa || !ob || !ow)) HDB_THROW(HDB_EINVAL, "bad arguments");
+        Stager s(ctx);
+        const int32_t *da = s.in(va, ne), *db = s.in(vb, ne);
+        const double *dw = s.in(w, ne);
+        int32_t *xa = s.out(oa, ne), *xb = s.out(ob, ne);
+        double *xw = s.out(ow, ne);
+        merge_sorted_runs_device(ctx, da, db, dw, off, xa, xb, xw);
+        s.finish();
+    });
+}
+
 int hdb_local_mst_ids(hdb_ctx *ctx, const int32_t *ids, int64_t n, const int32_t *va, const int32_t *vb,
                       const double *w, int64_t ne, int32_t node, int32_t *fake1, int32_t *fake2, int32_t *node_out) {
     return guarded(ctx, [&] {

@@ -41,6 +41,8 @@ void bubble_knn_device(hdb_ctx *ctx, const double *rep, const double *eB, const 
                        int metric, int K, double *knn_out, int32_t *log_out);
 void sort_edges_desc_device(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne);
 // CreateLocalMST record fields: local indices of each edge's vertices in `ids` (synchronises)
+void merge_sorted_runs_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, const double *w,
+                              const std::vector<int64_t> &off, int32_t *oa, int32_t *ob, double *ow);
 void local_mst_ids_device(hdb_ctx *ctx, const int32_t *ids, int64_t n, const int32_t *va, const int32_t *vb,
                           const double *w, int64_t ne,
                           int32_t node, int32_t *fake1, int32_t *fake2, int32_t *node_out);

@@ -193,6 +193,134 @@ void sort_edges_desc_device(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, i
     HIP_CHECK(hipGetLastError());
 }
 
+// ------------------------------------------------ merge of presorted runs
+// Stable merge of two descending runs A, B (A first on equal weights) by merge-path tiles:
+// a workgroup finds where its MP_T outputs start in A and B (one diagonal binary search per
+// end), stages both slices' weights in LDS, and every thread places its outputs with a binary
+// search inside the tile.
+constexpr int MP_T = 1024, MP_TB = 256;
+__device__ __forceinline__ int64_t mp_split(const double *wA, int64_t na, const double *wB, int64_t nb, int64_t k) {
+    int64_t lo = k - nb > 0 ? k - nb : 0, hi = k < na ? k : na;
+    while (lo < hi) {  // the number of A elements among the first k outputs
+        const int64_t mid = (lo + hi) >> 1;
+        if (wA[mid] >= wB[k - mid - 1]) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(MP_TB) void merge_path_kernel(const int32_t *__restrict__ aA, const int32_t *__restrict__ bA,
+                                                         const double *__restrict__ wA, int64_t na,
+                                                         const int32_t *__restrict__ aB, const int32_t *__restrict__ bB,
+                                                         const double *__restrict__ wB, int64_t nb,
+                                                         int32_t *__restrict__ oa, int32_t *__restrict__ ob,
+                                                         double *__restrict__ ow) {
+    __shared__ double sw[2 * MP_T];
+    __shared__ int64_t s_i[2];
+    const int64_t k0 = (int64_t)blockIdx.x * MP_T, k1 = min(k0 + MP_T, na + nb);
+    if (threadIdx.x < 2) s_i[threadIdx.x] = mp_split(wA, na, wB, nb, threadIdx.x ? k1 : k0);
+    __syncthreads();
+    const int64_t i0 = s_i[0], j0 = k0 - i0, i1 = s_i[1], j1 = k1 - i1;
+    const int nA = (int)(i1 - i0), nB = (int)(j1 - j0);
+    for (int t = threadIdx.x; t < nA; t += MP_TB) sw[t] = wA[i0 + t];
+    for (int t = threadIdx.x; t < nB; t += MP_TB) sw[nA + t] = wB[j0 + t];
+    __syncthreads();
+    const int cnt = (int)(k1 - k0);
+    for (int t = threadIdx.x; t < cnt; t += MP_TB) {
+        int lo = t - nB > 0 ? t - nB : 0, hi = t < nA ? t : nA;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sw[mid] >= sw[nA + t - mid - 1]) lo = mid + 1;
+            else hi = mid;
+        }
+        const int i = lo, j = t - lo;
+        const bool takeA = j >= nB || (i < nA && sw[i] >= sw[nA + j]);
+        const int64_t k = k0 + t;
+        if (takeA) {
+            oa[k] = aA[i0 + i];
+            ob[k] = bA[i0 + i];
+            ow[k] = sw[i];
+        } else {
+            oa[k] = aB[j0 + j];
+            ob[k] = bB[j0 + j];
+            ow[k] = sw[nA + j];
+        }
+    }
+}
+
+// precondition check: no NaN, every run non-increasing (bit 0 / bit 1)
+__global__ void runs_check_kernel(const double *__restrict__ w, int64_t ne, const int64_t *__restrict__ run_end_flag,
+                                  int *__restrict__ err) {
+    int e = 0;
+    HDB_GRID_STRIDE(i, ne) {
+        const double x = w[i];
+        if (x != x) e |= 1;
+        if (i + 1 < ne && !run_end_flag[i] && x < w[i + 1]) e |= 2;
+    }
+    if (e) atomicOr(err, e);
+}
+
+void merge_sorted_runs_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, const double *w,
+                              const std::vector<int64_t> &off, int32_t *oa, int32_t *ob, double *ow) {
+    hipStream_t st = ctx->stream;
+    const int nr = (int)off.size() - 1;
+    const int64_t ne = off.back();
+    if (ne <= 0) return;
+    KernelTimer t(ctx, "merge_runs");
+    // scratch: the ping-pong buffer, the run-end flags, the error word
+    const size_t sb = ((size_t)ne * 16 + 255) & ~size_t(255);
+    char *base = (char *)arena(ctx, A_WORK3, sb + (size_t)ne * 8 + 512);
+    int32_t *ta = (int32_t *)base, *tb_ = ta + ne;
+    double *tw = (double *)(base + (((size_t)ne * 8 + 255) & ~size_t(255)));
+    int64_t *flag = (int64_t *)(base + sb);
+    int *err = (int *)(flag + ne);
+    HIP_CHECK(hipMemsetAsync(flag, 0, (size_t)ne * 8 + 512, st));
+    std::vector<int64_t> ends;
+    for (int r = 0; r < nr; r++)
+        if (off[r + 1] > off[r]) ends.push_back(off[r + 1] - 1);
+    for (int64_t e : ends) HIP_CHECK(hipMemsetAsync(flag + e, 0xff, 8, st));
+    hipLaunchKernelGGL(runs_check_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(ne, 256), 8192)), dim3(256), 0, st,
+                       w, ne, flag, err);
+    // pairwise rounds; the last round writes the outputs
+    std::vector<int64_t> cur = off;
+    const int32_t *sa = va, *sbv = vb;
+    const double *sw = w;
+    int rounds = 0;
+    for (int k = 1; k < nr; k <<= 1) rounds++;
+    if (rounds == 0) {
+        HIP_CHECK(hipMemcpyAsync(oa, va, 4 * ne, hipMemcpyDeviceToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(ob, vb, 4 * ne, hipMemcpyDeviceToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(ow, w, 8 * ne, hipMemcpyDeviceToDevice, st));
+    }
+    for (int r = 0; r < rounds; r++) {
+        // the last round lands in the outputs; earlier ones alternate so the input is never overwritten
+        const bool last = r == rounds - 1;
+        int32_t *da = last ? oa : ((rounds - 1 - r) & 1 ? ta : oa);
+        int32_t *db = last ? ob : ((rounds - 1 - r) & 1 ? tb_ : ob);
+        double *dw = last ? ow : ((rounds - 1 - r) & 1 ? tw : ow);
+        std::vector<int64_t> nxt{0};
+        for (size_t p = 0; p + 1 < cur.size(); p += 2) {
+            const int64_t a0 = cur[p], a1 = cur[p + 1];
+            const int64_t b1 = p + 2 < cur.size() ? cur[p + 2] : a1;  // an odd run passes through
+            const int64_t na = a1 - a0, nb = b1 - a1;
+            if (na + nb > 0)
+                hipLaunchKernelGGL(merge_path_kernel, dim3((unsigned)ceil_div(na + nb, (int64_t)MP_T)), dim3(MP_TB), 0,
+                                   st, sa + a0, sbv + a0, sw + a0, na, sa + a1, sbv + a1, sw + a1, nb, da + a0, db + a0,
+                                   dw + a0);
+            nxt.push_back(b1);
+        }
+        cur = nxt;
+        sa = da;
+        sbv = db;
+        sw = dw;
+    }
+    int h = 0;
+    HIP_CHECK(hipMemcpyAsync(&h, err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (h & 1) HDB_THROW(HDB_EINVAL, "merge_sorted_runs: NaN weight");
+    if (h & 2) HDB_THROW(HDB_EINVAL, "merge_sorted_runs: a run is not sorted descending");
+}
+
 // ------------------------------------------------ CreateLocalMST record fields
 // fake1 / fake2 of CreateLocalMST's records (CreateLocalMST.java:242,266,276-285) are the
 // partition-local indices of an edge's two vertices: the position of the global id in the

@@ -187,3 +187,17 @@ def sort_edges_desc(va, vb, w, ctx=None):
     c = _ctx(a, ctx)
     A.check(A.lib().hdb_sort_edges_desc(c.h, a.p, b.p, ww.p, ww.obj.shape[0]), "sort_edges_desc")
     return a.obj, b.obj, ww.obj
+
+
+def merge_sorted_runs(va, vb, w, run_off, ctx=None):
+    """The same order as sort_edges_desc over a concatenation of runs that are each sorted
+    descending already (per-rank sort_edges_desc outputs): stable merge, run order on ties.
+    run_off: nruns + 1 offsets.  Returns new (va, vb, w) arrays of the input's kind."""
+    a, b, ww = A.Arr(va, np.int32), A.Arr(vb, np.int32), A.Arr(w, np.float64)
+    off = np.ascontiguousarray(np.asarray(run_off, np.int64))
+    ne = ww.obj.shape[0]
+    oa, ob, ow = A.new_like(a, (ne,), np.int32), A.new_like(a, (ne,), np.int32), A.new_like(a, (ne,), np.float64)
+    c = _ctx(a, ctx)
+    A.check(A.lib().hdb_merge_sorted_runs(c.h, a.p, b.p, ww.p, off.ctypes.data, len(off) - 1, A.ptr(oa), A.ptr(ob),
+                                          A.ptr(ow)), "merge_sorted_runs")
+    return oa, ob, ow

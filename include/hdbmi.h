@@ -91,7 +91,12 @@ int hdb_ctx_synchronize(hdb_ctx *ctx);
  *                                  stat "prim_coop_plain_retries" counts those fallbacks),
  *                                  "prim_coop_plain_spin_log2" (default 20: polls per exchange
  *                                  before the plain attempt reports non-co-residency),
- *                                  "prim_coop_slots" (exchange layout);
+ *                                  "prim_coop_xcd" (default 1: the plain attempt's working
+ *                                  workgroups, when the run-time XCC_ID check finds them on one
+ *                                  XCD, exchange through that XCD's L2 -- placement changes only
+ *                                  speed), "prim_coop_slots" (exchange layout);
+ *   "bubble_knn_split"(default 1): bubble core distances scan their candidates in chunks and
+ *                                  replay the sequential insertion log exactly;
  *   "boruvka_seed"    (default 1): a Boruvka round starts from the previous round's still
  *                                  valid per-point edges;
  *   "boruvka_knn_seed"(default 1): hdb_exact_mst seeds every Boruvka round from the k-NN
@@ -207,6 +212,17 @@ int hdb_quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne);
  * sort by DESCENDING weight of the concatenated local edge lists, in place (device radix
  * sort).  The cross-GPU all-gather feeding it runs over RCCL in the host layer. */
 int hdb_sort_edges_desc(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne);
+
+/* The same result when the concatenation is made of runs that are each already sorted
+ * descending (as hdb_sort_edges_desc returns them): runs r = [run_off[r], run_off[r+1]) of
+ * (va, vb, w), nruns of them; output (oa, ob, ow) = the stable descending sort of their
+ * concatenation -- equal weights keep run order, then their order inside the run.  The
+ * stable sort of a rank-major concatenation of raw lists equals this merge of the ranks'
+ * individually sorted lists, so a reducer merges instead of re-sorting (pairwise merge-path
+ * tiles, O(E log nruns)).  Outputs must not alias inputs.  HDB_EINVAL on a NaN weight or a
+ * run that is not descending.  Synchronises. */
+int hdb_merge_sorted_runs(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, const double *w, const int64_t *run_off,
+                          int32_t nruns, int32_t *oa, int32_t *ob, double *ow);
 
 /* ---------------------------------------------- cross-GPU merge over RCCL (§8(b), §8(e))
  * One communicator per rank (one process per GPU).  The caller moves the unique id from the

@@ -399,6 +399,40 @@ def test_sort_edges_desc_runs(pkg, oracle, p, r, levels):
         assert eq(ga, ra) and eq(gb, rb) and eq(gw, rw2) and np.array_equal(np.signbit(gw), np.signbit(rw2))
 
 
+@pytest.mark.parametrize("sizes,levels", [([300_000, 250_000, 1, 0, 180_000, 300_000, 7, 64_000], 25),
+                                          ([1_000_000, 1_000_000], 0), ([5_000, 3_000, 9_000], 2), ([12_345], 4)])
+def test_merge_sorted_runs_equals_stable_sort(pkg, oracle, sizes, levels):
+    """hdb_merge_sorted_runs: the ranks' individually sorted lists merged (merge-path tiles,
+    run order on ties) equal the stable descending sort of the raw rank-major concatenation --
+    heavy ties across runs, empty and one-edge runs, an odd run count, one run; and the
+    precondition errors"""
+    rng = np.random.default_rng(sum(sizes) + levels)
+    raw, srt = [], []
+    for k, m in enumerate(sizes):
+        w = (rng.integers(0, levels + 1, m) * 0.25) if levels else rng.uniform(0, 50, m)
+        a = rng.integers(0, 1 << 30, m).astype(np.int32)
+        b = rng.integers(0, 1 << 30, m).astype(np.int32)
+        raw.append((a, b, w))
+        t = tuple(torch.from_numpy(x.copy()).cuda() for x in (a, b, w))
+        srt.append(pkg.sort_edges_desc(*t))
+    off = np.r_[0, np.cumsum(sizes)]
+    cat = [torch.cat([s_[i] for s_ in srt]) for i in range(3)]
+    ga, gb, gw = (x.cpu().numpy() for x in pkg.merge_sorted_runs(*cat, off))
+    ra, rb, rw = oracle.merge_edges(raw)
+    assert eq(ga, ra) and eq(gb, rb) and eq(gw, rw)
+    ha, hb, hw = pkg.merge_sorted_runs(*(x.cpu().numpy() for x in cat), off)  # host arrays, staged
+    assert eq(ha, ra) and eq(hb, rb) and eq(hw, rw)
+    if sum(sizes) > 10:
+        bad = cat[2].clone()
+        bad[1] = bad[0] + 1.0  # run 0 no longer descending
+        with pytest.raises(pkg.HdbError):
+            pkg.merge_sorted_runs(cat[0], cat[1], bad, off)
+        bad = cat[2].clone()
+        bad[3] = float("nan")
+        with pytest.raises(pkg.HdbError):
+            pkg.merge_sorted_runs(cat[0], cat[1], bad, off)
+
+
 def test_sort_edges_desc_exact_mst_list_and_nan(pkg, oracle):
     """the exact leaf's own output (tree edges ascending, then self edges) and a NaN weight
     (the run path is skipped: the radix order of NaN keys is kept)"""
