@@ -116,6 +116,49 @@ class HdbComm:
             pass
 
 
+def gather_sorted_msts(va, vb, w, dst: int = 0, group=None):
+    """The reducers' merge when every rank already holds its own list sorted (stable,
+    descending -- the order SortMST gives it): gather the blocks in rank order to `dst` only
+    (UnionFindReducer runs as one reducer, Main.java:302-347) and merge them there as presorted
+    runs (hdb_merge_sorted_runs: lower rank first on equal weights).  Equal to
+    merge_local_msts on the unsorted blocks -- a stable sort of a concatenation is the stable
+    merge of its stably sorted runs -- without the re-sort of the whole list.  Returns the
+    merged (va, vb, w) on `dst`, None on the other ranks."""
+    import torch
+    import torch.distributed as dist
+    world, rank = world_rank(group)
+    dev = _coll_device(group)
+    n = torch.tensor([w.shape[0]], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    m = max(counts) if counts else 0
+    out = []
+    for t in (va, vb, w):
+        src = t.to(dev)
+        if src.shape[0] != m:  # equal block sizes (the usual case) go without a pad copy
+            pad = torch.zeros(m, dtype=src.dtype, device=dev)
+            pad[: src.shape[0]] = src
+            src = pad
+        big = torch.empty(world * m, dtype=src.dtype, device=dev) if rank == dst else None
+        dist.gather(src, list(big.split(m)) if big is not None else None, dst=dst, group=group)
+        out.append(big)
+    if rank != dst:
+        return None
+    if m * world != sum(counts):
+        keep = torch.cat([torch.arange(r * m, r * m + c) for r, c in enumerate(counts)]).to(dev)
+        out = [x[keep] for x in out]
+    out = [x.to(w.device) for x in out]
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    if out[2].device.type == "cuda":
+        from .databubbles import merge_sorted_runs
+        return merge_sorted_runs(out[0], out[1], out[2], off)
+    # CPU tensors (gloo tests): the stable descending order of the concatenation (-0.0 == 0.0)
+    key = np.where(out[2].numpy() == 0.0, 0.0, out[2].numpy())
+    o = torch.from_numpy(np.argsort(-key, kind="stable"))
+    return out[0][o], out[1][o], out[2][o]
+
+
 def _merge_via_comm(comm: HdbComm, va, vb, w, seq):
     import torch
     ctx = comm.ctx

@@ -22,7 +22,9 @@ import argparse
 import importlib
 import json
 import os
+import queue
 import sys
+import threading
 import time
 
 import numpy as np
@@ -466,6 +468,8 @@ def main():
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2 (default): the per-GPU C2 pipeline (weak scaling); c3/c5: the whole "
                          "partitioned job over the sharded driver (strong scaling)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process group for N>1 (gloo: rehearse several ranks on one device)")
     ap.add_argument("--phases", action="store_true", help="c3/c5: per-phase times (synchronising)")
     args = ap.parse_args()
     if args.steps is None:
@@ -483,8 +487,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":
+        local = 0  # rehearsal: every rank on device 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group(args.backend, **({"device_id": torch.device("cuda", local)}
+                                                 if args.backend == "nccl" else {}))
     torch.cuda.set_device(local)
     pkg = importlib.import_module(PKG)
     par = importlib.import_module(PKG + ".parallel")
@@ -511,34 +518,122 @@ def main():
         return mst.getVerticeA(), mst.getVericeB(), mst.getEges()
 
     def merge(va, vb, w):
+        """the reducers' merge: N=1 sorts the list; N>1 sorts each rank's own list (also the
+        input of its partition's labels) and merges the presorted runs on rank 0 only"""
+        va, vb, w = pkg.sort_edges_desc(va, vb, w, ctx)
         if world > 1:
-            return par.merge_local_msts(va, vb, w)
-        return pkg.sort_edges_desc(va, vb, w, ctx)
+            return (va, vb, w), par.gather_sorted_msts(va, vb, w, dst=0)
+        return (va, vb, w), (va, vb, w)
 
     def step_e2e():
         X_dev.copy_(X_pin, non_blocking=True)                    # H2D
-        va, vb, w = leaf(X_dev)
-        if world > 1:                                            # label this partition
-            la, lb, lw = pkg.sort_edges_desc(va.clone(), vb.clone(), w.clone(), ctx)
-            lab, n_clusters[0] = pkg.flat_labels(la, lb, lw, n, MIN_CL_SIZE, ctx=ctx)
-            ma, mb, mw = merge(va, vb, w)
-        else:
-            ma, mb, mw = merge(va, vb, w)
+        own, merged = merge(*leaf(X_dev))
         main = torch.cuda.current_stream()
         if rank == 0:  # D2H of the merged list on a copy stream, overlapping the labels
+            ma, mb, mw = merged
             copy_s.wait_stream(main)
             with torch.cuda.stream(copy_s):
                 va_h.copy_(ma, non_blocking=True)
                 vb_h.copy_(mb, non_blocking=True)
                 w_h.copy_(mw, non_blocking=True)
-        if world == 1:
-            lab, n_clusters[0] = pkg.flat_labels(ma, mb, mw, n, MIN_CL_SIZE, ctx=ctx)
+        lab, n_clusters[0] = pkg.flat_labels(*own, n, MIN_CL_SIZE, ctx=ctx)  # this partition's labels
         lab_h.copy_(lab, non_blocking=True)
         main.synchronize()
         copy_s.synchronize()
 
+    class LabelStage:
+        """Stage 2 of the step pipeline, on its own thread, HIP stream and library context:
+        partition i's K6 flat labels and the D2H of its merged list and labels run while the
+        main thread runs partition i+1's H2D, MST and merge (the library's ctypes calls release
+        the GIL).  Every step still does all of its work; the timer stops after the last
+        step's stage 2 has finished."""
+
+        def __init__(self):
+            self.q = queue.Queue(maxsize=1)
+            self.err = None
+            self.ready = threading.Event()
+            self.t = threading.Thread(target=self._run, daemon=True)
+            self.t.start()
+            self.ready.wait()
+
+        def _run(self):
+            torch.cuda.set_device(local)
+            prio = int(os.environ.get("HDB_BENCH_STAGE2_PRIO", "0"))  # A/B knob: -1 = high priority
+            s, cs = torch.cuda.Stream(priority=prio), torch.cuda.Stream(priority=prio)
+            with torch.cuda.stream(s):
+                self.ctx = pkg.Context.get(local)  # thread-local: a second context
+                self.ctx.use_torch_stream()
+                self.ready.set()
+                while True:
+                    job = self.q.get()
+                    if job is None:
+                        self.q.task_done()
+                        return
+                    try:
+                        ev, own, merged = job
+                        s.wait_event(ev)
+                        if merged is not None:  # rank 0: D2H of the merged list beside the labels
+                            cs.wait_event(ev)
+                            with torch.cuda.stream(cs):
+                                va_h.copy_(merged[0], non_blocking=True)
+                                vb_h.copy_(merged[1], non_blocking=True)
+                                w_h.copy_(merged[2], non_blocking=True)
+                        lab, k = pkg.flat_labels(*own, n, MIN_CL_SIZE, ctx=self.ctx)
+                        lab_h.copy_(lab, non_blocking=True)
+                        s.synchronize()
+                        cs.synchronize()
+                        n_clusters[0] = k
+                    except BaseException as e:  # re-raised on the main thread
+                        self.err = e
+                    finally:
+                        job = own = merged = lab = None
+                        self.q.task_done()
+
+        def submit(self, own, merged):
+            if self.err is not None:
+                raise self.err
+            ev = torch.cuda.Event()
+            ev.record()  # the main stream's MST + merge of this partition
+            self.q.put((ev, own, merged))
+
+        def drain(self):
+            self.q.join()
+            if self.err is not None:
+                raise self.err
+
+        def close(self):
+            self.q.put(None)
+            self.t.join()
+
+    stage = LabelStage()
+    # H2D of step i+1's points on a copy stream during step i's MST (two point buffers)
+    X_bufs = [X_dev, torch.empty_like(X_dev)]
+    h2d_s = torch.cuda.Stream()
+    h2d_ev = [None, None]
+    pipe = {"next": 0, "end": 0}
+
+    def prefetch(j):
+        h2d_s.wait_stream(torch.cuda.current_stream())  # buffer j % 2's last reader (step j - 2) is queued before
+        with torch.cuda.stream(h2d_s):
+            X_bufs[j % 2].copy_(X_pin, non_blocking=True)
+            h2d_ev[j % 2] = torch.cuda.Event()
+            h2d_ev[j % 2].record()
+
+    def pipe_run(steps):
+        """`steps` pipelined steps; returns when the last one's labels are on the host"""
+        i0 = pipe["next"]
+        prefetch(i0)
+        for i in range(i0, i0 + steps):
+            torch.cuda.current_stream().wait_event(h2d_ev[i % 2])
+            if i + 1 < i0 + steps:
+                prefetch(i + 1)
+            own, merged = merge(*leaf(X_bufs[i % 2]))
+            stage.submit(own, merged if rank == 0 else None)
+        pipe["next"] = i0 + steps
+        stage.drain()
+
     def step_dev():
-        return merge(*leaf(X_res))
+        return merge(*leaf(X_res))[1]
 
     def barrier():
         if world > 1:
@@ -546,28 +641,39 @@ def main():
         torch.cuda.synchronize()
 
     def max_over_ranks(x):
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64, device="cuda" if args.backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    for _ in range(args.warmup):
-        step_e2e()
+    pipe_run(args.warmup)
     barrier()
-    # per-kernel device times: HIP events recorded on the launch stream inside the timed
+    # per-kernel device times: HIP events recorded on the launch streams inside the timed
     # region (measured cost of the records: ~1% of a step)
-    keys = ("knn_tree", "boruvka_total", "boruvka_scan", "merge_sort", "flat_labels")
-    ctx.set_timing(True)
+    keys = ("knn_tree", "boruvka_total", "boruvka_scan", "merge_sort")
+    for c in (ctx, stage.ctx):
+        c.set_timing(True)
     for k in keys:
         ctx.kernel_time(k)
+    stage.ctx.kernel_time("flat_labels")
+    barrier()
+    t0 = time.perf_counter()
+    pipe_run(args.steps)
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    for c in (ctx, stage.ctx):
+        c.set_timing(False)
+    kt = {k: ctx.kernel_time(k) for k in keys}
+    kt["flat_labels"] = stage.ctx.kernel_time("flat_labels")
+    stage.close()
+    # latency of one step without the pipeline (each step's stages back to back)
+    step_e2e()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step_e2e()
     barrier()
-    dt = max_over_ranks(time.perf_counter() - t0)
-    ctx.set_timing(False)
-    kt = {k: ctx.kernel_time(k) for k in keys}
+    dt_lat = max_over_ranks(time.perf_counter() - t0)
     # the same pipeline from HBM-resident points to HBM-resident merged edges
     step_dev()
     barrier()
@@ -643,10 +749,15 @@ def main():
         "config": {"workload": "config 2: blobs 1M x 3 exact HDBSCAN* (no sampling), minPts 4, minClSize 4",
                    "points_per_gpu": n, "d": D, "min_pts": MIN_PTS, "min_cl_size": MIN_CL_SIZE,
                    "core": "EXCL_SELF", "timed": "pinned host X -> H2D -> K1t cores -> K2b MST + self edges "
-                   "-> merge sort -> K6 flat labels (D2H of the merged list overlapping it on a copy "
-                   "stream) -> D2H of the labels",
+                   "-> merge sort (N>1: per-rank sort, gather to rank 0, merge of the presorted runs) -> "
+                   "K6 flat labels of the partition (D2H of the merged list overlapping it on a copy "
+                   "stream) -> D2H of the labels; pipelined: step i's labels + D2H (own thread, stream and "
+                   "library context) and step i+1's H2D (copy stream) overlap step i+1's / i's MST + merge; "
+                   "the timer starts before step 1's H2D and stops after the last step's labels are on the host",
                    "parallelism": f"partition-sharded x{world}"},
         "n_clusters": n_clusters[0],
+        "latency_ms_per_step": dt_lat * 1e3 / tsteps,
+        "latency_kind": "the same steps without the pipeline: each step's stages back to back",
         "device_resident_points_per_s": total_points * tsteps / dt_dev,
         "device_resident_ms_per_step": dt_dev * 1e3 / tsteps,
         "mrd_evals_per_s": evals * tsteps / dt,

@@ -129,3 +129,12 @@ def test_hdb_merge_edges_rccl_world1(oracle, tmp_path):
     assert np.array_equal(z["a"], ref[0]) and np.array_equal(z["b"], ref[1]) and np.array_equal(z["ww"], ref[2])
     ref2 = oracle.merge_edges([(z["va"], z["vb"], z["w"])])
     assert np.array_equal(z["a2"], ref2[0]) and np.array_equal(z["b2"], ref2[1]) and np.array_equal(z["w2"], ref2[2])
+
+
+def test_gather_sorted_msts_merges_on_device(oracle):
+    """gather_sorted_msts with HIP tensors (2 and 3 ranks on the box's one device, gloo carries
+    the blocks): rank 0 merges the presorted runs with hdb_merge_sorted_runs -> the oracle's
+    SortMST order of the rank-major concatenation, ragged and empty blocks included"""
+    from test_distributed import _check_gather
+    for world in (2, 3):
+        _check_gather(oracle, world, "cuda")
