@@ -15,7 +15,9 @@ oracle for the parity tests):
           batched call for all leaves <= LEAF_PRIM_MAX points (and for any size when
           exact_prim_leaves is set or K2b does not apply: other metrics, other d); larger
           forced leaves use hdb_exact_mst: the same cores + Boruvka on one index (exact
-          weights; topology differs from Prim only on ties)
+          weights; topology differs from Prim only on ties).  Leaves are end points of
+          the subset tree, so they are deferred (defer_leaves): every level's leaves run as
+          one batch after the level loop (identical blocks, placed by their canonical ids)
   big subsets: D2 samples -> keyed nearest sample (FirstStep.java:74-85, D3) -> bulk
           CombineStep (D5 fold order) -> per subset LocalModelReduceByKey (D4) -> partition
           induction (Main.java:272-289, including the in-place relabel) -> LabelClassification
@@ -23,7 +25,7 @@ oracle for the parity tests):
 
 Multi-GPU (one process per GPU, torch.distributed initialised, X given to
 every rank): the plan is computed identically on every rank -- leaves go to ranks by LPT on
-n_i^2, the big subsets' points are split in contiguous chunks for the nearest-sample scan (the
+n_i^2 (over the whole job when deferred, per level otherwise), the big subsets' points are split in contiguous chunks for the nearest-sample scan (the
 assignments are all-gathered), bubble statistics are recomputed on every rank (the D5 fold
 order keeps them bit-exact), local models go to ranks by LPT on b_i^2 (results all-gathered
 and applied in subset order), and the merge places every local edge at its position in the
@@ -68,7 +70,7 @@ class MRHDBSCANStar:
     def __init__(self, minPts=4, minClSize=4, processing_units=50, k=0.2, samples_per_subset=None,
                  seed=20210101, distanceFunction=None, all_inter_edges=True, max_levels=64, ctx=None,
                  device=0, flat_labels=True, profile=False, exact_prim_leaves=False, group=None,
-                 prim_leaf_max=LEAF_PRIM_MAX, model_threads=4):
+                 prim_leaf_max=LEAF_PRIM_MAX, model_threads=4, defer_leaves=True):
         self.minPts = minPts
         self.minClSize = minClSize
         self.processing_units = processing_units
@@ -93,6 +95,11 @@ class MRHDBSCANStar:
         # a level's local models run concurrently, one host thread (own context and stream)
         # each: a bubble Prim occupies only ceil(b / 1024) CUs
         self.model_threads = int(os.environ.get("HDB_MODEL_THREADS", model_threads))
+        # leaves are end points of the subset tree: nothing later in the loop reads their edges,
+        # so they can wait until the level loop is done and then run as ONE batch over the
+        # whole job (global LPT over the ranks, one batched Prim launch for every small leaf)
+        # instead of one synchronising batch per level -- the same blocks, the same result
+        self.defer_leaves = defer_leaves
         self._pool = None
         self.group = group      # torch.distributed group (None: the default group, if any)
         self._comm = None       # HdbComm for the merge under nccl
@@ -236,6 +243,7 @@ class MRHDBSCANStar:
         forced = set()
         leaf_of = torch.full((n,), -1, dtype=torch.int64, device=dev)
         blocks, block_size, levels = [], {}, []  # blocks: (canonical id, edges) computed here
+        pending = []  # deferred leaves: (canonical block id, rows)
         iteration, processed, next_id = 0, 0, 2  # Main.java:103-105
         while processed < n:
             # group the alive records by (key, global id) -- D5
@@ -259,7 +267,12 @@ class MRHDBSCANStar:
             if self.profile:
                 self._lvl = {"phase_s": {}}
                 self.level_tasks.append(self._lvl)
-            if leaf_k:
+            if leaf_k and self.defer_leaves:
+                for i, (kk, r) in enumerate(zip(leaf_k, leaf_rows)):
+                    block_size[(iteration, 0, i)] = 2 * int(r.shape[0]) - 1
+                    leaf_of[r] = kk
+                    pending.append(((iteration, 0, i), r))
+            elif leaf_k:
                 self._mark("bookkeeping")
                 owner = P.lpt([int(r.shape[0]) ** 2 for r in leaf_rows], world)
                 mine = [i for i in range(len(leaf_k)) if owner[i] == rank]
@@ -395,6 +408,19 @@ class MRHDBSCANStar:
             alive = brows
             levels.append(level)
         self._mark("bookkeeping")
+        if pending:
+            # every level's leaves in one batch: LPT over the ranks on n^2 across the whole job
+            # (a level with one big leaf no longer idles the other ranks)
+            if self.profile:
+                self._lvl = {"phase_s": {}, "deferred_leaves": True}
+                self.level_tasks.append(self._lvl)
+            owner = P.lpt([int(r.shape[0]) ** 2 for _, r in pending], world)
+            mine = [j for j in range(len(pending)) if owner[j] == rank]
+            if mine:
+                got = self._leaves(X, [pending[j][1] for j in mine], list(range(len(mine))))
+                blocks.extend((pending[j][0], e) for j, e in zip(mine, got))
+            if self.profile:
+                self._lvl["phase_s"]["leaves"] = self._mark("leaves")
         # UnionFindReducer + SortMST: stable descending sort of the iteration-major
         # concatenation (leaf blocks in key order, then the level's inter-cluster blocks)
         order = sorted(block_size)

@@ -313,7 +313,9 @@ def predicted_scaling(drv, par, ns=(1, 2, 4, 8)):
     durations of its tasks x (phase wall time / summed task time at N = 1: the concurrency the
     model threads reach on one GPU), the phase = its slowest rank; the point-chunked nearest
     sample scales as 1/N; bubbles (recomputed on every rank), bookkeeping, the merge and the
-    flat labels do not scale.  Not modelled: the all-gathers and the RCCL merge exchange."""
+    flat labels do not scale.  The driver's deferred leaves (every level's leaves in one
+    batch after the level loop) are one more "level" holding only leaves, so their LPT runs
+    over the whole job.  Not modelled: the all-gathers and the RCCL merge exchange."""
     fixed = sum(v for k, v in drv.timings.items() if k in ("bookkeeping", "merge", "flat_labels"))
     out, per = {}, {}
     for N in ns:
@@ -336,7 +338,8 @@ def predicted_scaling(drv, par, ns=(1, 2, 4, 8)):
             tot["bubbles"] += ph.get("bubbles", 0.0)
         per[N] = {k: round(v, 3) for k, v in tot.items()} | {"fixed": round(fixed, 3)}
         out[N] = sum(tot.values()) + fixed
-    return {"model": "LPT makespan of the measured N=1 task durations per level (leaves, local models), "
+    return {"model": "LPT makespan of the measured N=1 task durations per level (local models; leaves "
+                     "deferred: one LPT over the whole job), "
                      "nearest sample / N, bubbles + bookkeeping + merge + flat labels unscaled; "
                      "all-gathers and the RCCL merge exchange not modelled",
             "seconds": {str(N): round(v, 3) for N, v in out.items()},

@@ -82,3 +82,19 @@ def test_flat_labels_device_inputs(pkg, oracle):
     lab, k = pkg.flat_labels(va, vb, w, X.shape[0], 10)
     ref, kr = flat_labels(X.shape[0], va.cpu().numpy(), vb.cpu().numpy(), w.cpu().numpy(), 10)
     assert k == kr and np.array_equal(lab.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("name,pu,k", [("blobs8k_d8", 1500, 0.02), ("skin3k", 300, 0.1)])
+def test_deferred_leaves_equal_per_level_leaves(pkg, name, pu, k):
+    """defer_leaves (the default: every level's leaves in one batch after the level loop, one
+    LPT over the job) places the same blocks as the per-level leaf batches (Main.java:133-138
+    runs a level's leaves inside the level; nothing later reads their edges)."""
+    X = {"skin3k": lambda: load_skin(3000), "blobs8k_d8": lambda: blobs(8000, 8, 10, 2, spread=30.0)}[name]()
+    kw = dict(processing_units=pu, k=k)
+    a = pkg.MRHDBSCANStar(**kw, defer_leaves=True).run(X)
+    b = pkg.MRHDBSCANStar(**kw, defer_leaves=False).run(X)
+    assert a["iterations"] == b["iterations"]
+    assert np.array_equal(a["leaf_of"].cpu().numpy(), b["leaf_of"].cpu().numpy())
+    for x, y in zip(a["edges"], b["edges"]):
+        assert np.array_equal(x.cpu().numpy(), y.cpu().numpy())
+    assert np.array_equal(a["labels"].cpu().numpy(), b["labels"].cpu().numpy())
