@@ -97,7 +97,7 @@ namespace hdb {
 // scratch slot ids
 enum {
     A_STAGE_IN = 0, A_STAGE_OUT = 1, A_WORK0 = 2, A_WORK1 = 3, A_WORK2 = 4, A_WORK3 = 5, A_PAD = 6, A_SORT = 7,
-    A_FLAT0 = 8, A_FLAT1 = 9, A_FLAT_TMP = 10, A_LOG = 11, A_ORDER = 12
+    A_FLAT0 = 8, A_FLAT1 = 9, A_FLAT_TMP = 10, A_LOG = 11, A_ORDER = 12, A_SBKEY = 13
 };
 
 void *arena(hdb_ctx *ctx, int slot, size_t bytes);

@@ -364,6 +364,21 @@ constexpr int NW = HDB_K1S_WAVES;
 #ifndef HDB_K1S_XCD
 #define HDB_K1S_XCD 1  // contiguous query-group ranges per XCD (A/B at C4: screen 51.8 -> 50.7 ms)
 #endif
+#ifndef HDB_K1S_REGTOP
+// 1: each lane keeps the running top-KC upper bounds of its (query, half-wave) pair in
+// registers and logs into its own half of the query's log, so the two half-waves of a wave
+// take their hits at the same time and an insertion is a register network instead of a
+// dependent LDS shift chain (KC <= 15).  The query's threshold is the KC-th smallest bound of
+// the union of its two halves' lists (the halves see disjoint candidate rows, so the union
+// holds bounds of distinct candidates: >= the KC-th exact value), refreshed per hit step
+#define HDB_K1S_REGTOP 1
+#endif
+#ifndef HDB_K1S_SBKEYS
+#define HDB_K1S_SBKEYS 1  // superblock visiting keys of all groups in one grid up front (sb_keys_kernel)
+#endif
+#ifndef HDB_K1S_PROF
+#define HDB_K1S_PROF 0  // diagnostic build: per-wave cycle split of the screen loop (stats k1s_prof_*)
+#endif
 #ifndef HDB_K1F_COMPACT
 #define HDB_K1F_COMPACT 1  // re-check: compact the surviving log entries first (A/B at C4: 23.6 -> 16.3 ms)
 #endif
@@ -378,7 +393,7 @@ __device__ __forceinline__ int64_t xcd_contig(int64_t b, int64_t G) {
     return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
 }
 #ifndef HDB_K1S_WPE
-#define HDB_K1S_WPE (HDB_K1S_QT == 1 ? 4 : 2)
+#define HDB_K1S_WPE (HDB_K1S_QT == 1 ? (HDB_K1S_REGTOP ? 3 : 4) : 2)
 #endif
 constexpr int K1S_WPE = HDB_K1S_WPE;  // waves per SIMD (A/B at C4: 4 = two workgroups per CU, 51.7 ms, despite
                                       // spilling some fragments; 3 = 168 VGPRs without spills, one workgroup, 57.0 ms)
@@ -415,10 +430,10 @@ __global__ void screen_consts_kernel(const double *__restrict__ nrm2, const doub
     }
 }
 
-// the log of one query is full: keep the entries that can still matter (lb <= thr)
-__device__ __noinline__ int log_compact(LogEnt *L, float t) {
+// the log of one query (or half-query) is full: keep the entries that can still matter (lb <= thr)
+__device__ __noinline__ int log_compact(LogEnt *L, float t, int cap = S_LOGCAP) {
     int w = 0;
-    for (int j = 0; j < S_LOGCAP; j++) {
+    for (int j = 0; j < cap; j++) {
         const LogEnt e = L[j];
         if (e.lb <= t) L[w++] = e;
     }
@@ -606,7 +621,63 @@ struct SbArgs {
     int nsb;                   // superblocks (<= NSB_MAX)
     int prune;                 // 0: every superblock in index order
     unsigned long long *blocks_done;
+    const float *keys;         // [groups][nsbp] visiting keys from sb_keys_kernel (null: in the screen)
 };
+
+// The superblock visiting keys of every (query group, superblock) pair, computed up front in
+// one grid: a workgroup takes 16 groups x 64 superblocks, their ball centres staged in LDS
+// 32 dimensions at a time, each thread 4 groups of one superblock; the squared centre
+// distance sums the dimensions in index order (the order the screen's own setup used).
+// The screen kernel then only reads its group's row (coalesced) before sorting it.
+template <int DP>
+__global__ __launch_bounds__(256) void sb_keys_kernel(const double *__restrict__ qctr, const double *__restrict__ qrn,
+                                                      const double *__restrict__ sctr, const double *__restrict__ srn,
+                                                      int64_t ngroups, int nsb, int nsbp, double eps_dot,
+                                                      float *__restrict__ keys) {
+    constexpr int TG = 16, TS = 64, DC = 32;
+    __shared__ double q_s[TG][DC + 1], s_s[TS][DC + 1];
+    const int tid = threadIdx.x, si = tid & (TS - 1), gq = (tid >> 6) * 4;
+    const int64_t g0 = (int64_t)blockIdx.y * TG;
+    const int s0 = blockIdx.x * TS;
+    double d2[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int c0 = 0; c0 < DP; c0 += DC) {
+        for (int i = tid; i < TG * DC; i += 256) {
+            const int r = i / DC, c = i % DC;
+            q_s[r][c] = g0 + r < ngroups ? qctr[(g0 + r) * DP + c0 + c] : 0.0;
+        }
+        for (int i = tid; i < TS * DC; i += 256) {
+            const int r = i / DC, c = i % DC;
+            s_s[r][c] = s0 + r < nsb ? sctr[(int64_t)(s0 + r) * DP + c0 + c] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int c = 0; c < DC; c++) {
+            const double sv = s_s[si][c];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const double e = q_s[gq + u][c] - sv;
+                d2[u] += e * e;
+            }
+        }
+        __syncthreads();
+    }
+    const int i = s0 + si;
+    if (i >= nsbp) return;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int64_t g = g0 + gq + u;
+        if (g >= ngroups) continue;
+        float key = INFINITY;
+        if (i < nsb) {
+            const double RQ = qrn[2 * g], NQ = qrn[2 * g + 1], RS = srn[2 * i], NS = srn[2 * i + 1];
+            const double gap = sqrt(d2[u]) * (1.0 - 1e-12) - (RQ + RS) * (1.0 + 1e-12);
+            const double lb2 = gap > 0.0 ? gap * gap * (1.0 - 1e-12) : 0.0;
+            const double bm = eps_dot * NQ * NS + 4e-13 * (NQ * NQ + NS * NS) + 1e-30;
+            key = f32_down(lb2 - 2.0 * bm * (1.0 + 1e-12));
+        }
+        keys[g * nsbp + i] = key;
+    }
+}
 
 template <int DP, int KC>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE, K1S_WPE))) void knn_mfma_screen_kernel(
@@ -630,8 +701,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
         if constexpr (decltype(B)::value == 0) return cst0_s;
         else return cst1_s;
     };
-    __shared__ float top_s[SQ * KC];
-    __shared__ int cnt_s[SQ];
+    constexpr bool REG = HDB_K1S_REGTOP && KC <= 15;  // register lists (see HDB_K1S_REGTOP)
+    static_assert(!REG || QT == 1, "register top lists hold one query per lane");
+    constexpr int LH = S_LOGCAP / 2;  // REG: entries per half-query log
+    constexpr int KR = REG ? KC : 1, KT = KR - 1;  // register list length, its last slot
+    __shared__ float top_s[REG ? 1 : SQ * KC];
+    __shared__ int cnt_s[REG ? 1 : SQ];
     __shared__ double qn2_s[SQ], qn_s[SQ];
 
     __shared__ float sk_s[NSB_MAX];           // superblock keys (lower bound - 2 max bound), ascending
@@ -639,7 +714,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     __shared__ int sbs_s[NSB_MAX];            // first block of the i-th superblock in key order
     __shared__ float tmax_s[2][NW];           // per-wave max thr, written in alternate iterations
 
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, half = lane >> 5, col = lane & 31;
+    // the wave index as a scalar: the LDS-DMA destinations (M0) and buffer resources derived
+    // from it stay in SGPRs (no waterfall loop, no VGPRs spent on uniform addresses)
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63,
+              half = lane >> 5, col = lane & 31;
+#if HDB_K1S_PROF
+    const uint64_t p_t0 = __builtin_readcyclecounter();
+    uint64_t p_wait = 0, p_mfma = 0, p_hit = 0, p_hitsteps = 0, p_hits = 0, p_setup = 0;
+#endif
 #if K1S_XCD
     // query groups of one k-means cluster are consecutive and visit the same candidate
     // superblocks: give each XCD (workgroups are dealt round-robin over the 8) a contiguous
@@ -654,7 +736,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
         bool any = false;
         for (int i = 0; i < SQ && !any; i += 32) any = sb.perm[qbase + i] >= 0;
         if (!any) {
-            for (int i = tid; i < SQ; i += 64 * NW) log_cnt[qbase + i] = 0;
+            for (int i = tid; i < (REG ? 2 : 1) * SQ; i += 64 * NW) log_cnt[(REG ? 2 : 1) * qbase + i] = 0;
             return;
         }
     }
@@ -662,9 +744,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     const float epsf = (float)eps_dot * 1.001f;
     const bool ex = excl != 0;
 
-    for (int i = tid; i < SQ * KC; i += 64 * NW) top_s[i] = INFINITY;
+    if constexpr (!REG)
+        for (int i = tid; i < SQ * KC; i += 64 * NW) top_s[i] = INFINITY;
     for (int i = tid; i < SQ; i += 64 * NW) {
-        cnt_s[i] = 0;
+        if constexpr (!REG) cnt_s[i] = 0;
         qn2_s[i] = nrm2[qbase + i];
         qn_s[i] = nrm[qbase + i];
     }
@@ -674,6 +757,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     int nsbp = 1;
     while (nsbp < sb.nsb) nsbp <<= 1;
     if (sb.prune) {
+        if (sb.keys) {  // precomputed (sb_keys_kernel): one coalesced row
+            for (int i = tid; i < nsbp; i += 64 * NW) {
+                sk_s[i] = sb.keys[gid * nsbp + i];
+                si_s[i] = (unsigned short)i;
+            }
+        } else {
         const double *mq = sb.qctr + gid * DP;
         const double RQ = sb.qrn[2 * gid], NQ = sb.qrn[2 * gid + 1];
         for (int i = tid; i < nsbp; i += 64 * NW) {
@@ -693,6 +782,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
             }
             sk_s[i] = key;
             si_s[i] = (unsigned short)i;
+        }
         }
         __syncthreads();
         for (int k = 2; k <= nsbp; k <<= 1)
@@ -726,6 +816,24 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     // query t of this lane: row qbase + qloc(t) (recomputed: fewer live registers)
     auto qloc_of = [&](int t) { return wave * 32 * QT + 32 * t + col; };
     unsigned qvm = 0;  // bit t: a real row (not padding)
+    // REG: this lane's (query, half) running list of upper bounds (ascending), its half-log
+    // length (LH + 1: overflowed) and the query's threshold (KC-th bound of both halves' lists)
+    float tl[KR];
+#pragma unroll
+    for (int k = 0; k < KR; k++) tl[k] = INFINITY;
+    int lcnt = 0;
+    float thq = INFINITY;
+    // KC-th smallest of the union of this lane's list and its partner half's (lane ^ 32):
+    // min over i of max(A_(i), B_(KC-i)) with A_(0) = B_(0) = -inf
+    auto union_kth = [&]() __attribute__((always_inline)) {
+        float pv[KR];
+#pragma unroll
+        for (int k = 0; k < KR; k++) pv[k] = __shfl_xor(tl[k], 32);
+        float th = fminf(pv[KT], tl[KT]);
+#pragma unroll
+        for (int i = 1; i < KR; i++) th = fminf(th, fmaxf(tl[i - 1], pv[KT - i]));
+        return th;
+    };
 #pragma unroll
     for (int t = 0; t < QT; t++) {
         const int64_t row = qbase + qloc_of(t);
@@ -748,8 +856,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     constexpr int GW = (CH + NW - 1) / NW;  // wave-instructions per wave per block
     // buffer loads with a per-block SGPR resource and a 32-bit lane offset (no 64-bit
     // per-lane address registers)
-    auto stage = [&](auto B, int64_t cb) __attribute__((always_inline)) {
-        __bf16 *base = cbuf(B);
+    auto stage = [&](__bf16 *base, float *cdst, int64_t cb) __attribute__((always_inline)) {
         int lr = lane;
         asm volatile("" : "+v"(lr));  // recomputed, not held live across the loop
         const __amdgpu_buffer_rsrc_t rh =
@@ -769,7 +876,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
         if (wave == 0 && lane < S_CST / 4) {
             const __amdgpu_buffer_rsrc_t rc =
                 __builtin_amdgcn_make_buffer_rsrc((void *)(cst + (cb >> 5) * S_CST), (short)0, S_CST * 4, 0x00020000);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (lds_ptr_t)cstb(B), 16, lane * 16, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (lds_ptr_t)cdst, 16, lr * 16, 0, 0, 0);
         }
     };
 
@@ -782,10 +889,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     int par = 0;
     int ci_sb = 0, ci_b = 0;  // current superblock (key order) and block within it; -1: done
     int64_t nproc = 0;
-    auto step = [&](auto B, auto Bn) {
+    // One block step.  The current and the next buffers come in as __restrict__ parameters:
+    // inlining them gives the LDS-DMA stores into `nxt` and the ds_reads of `cur` disjoint
+    // alias scopes, which is what lets the compiler's waitcnt pass issue the MFMA operand reads
+    // without first draining the next block's DMA (two distinct LDS objects alone do not).
+    auto body = [&](const __bf16 *__restrict__ cur, __bf16 *__restrict__ nxt, const float *__restrict__ cstc,
+                    float *__restrict__ cstn) __attribute__((always_inline)) {
         const int64_t cb = ((int64_t)sbs_s[ci_sb] + ci_b) * 32;
+#if HDB_K1S_PROF
+        const uint64_t p_a = __builtin_readcyclecounter();
+#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // block landed everywhere; the other buffer is free
+#if HDB_K1S_PROF
+        const uint64_t p_b = __builtin_readcyclecounter();
+        p_wait += p_b - p_a;
+#endif
         float thrmax = tmax_s[par ^ 1][0];
 #pragma unroll
         for (int w = 1; w < NW; w++) thrmax = fmaxf(thrmax, tmax_s[par ^ 1][w]);
@@ -795,11 +914,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
             nx_b = 0;
             if (!(nx_sb < sb.nsb && sk_s[nx_sb] <= thrmax)) nx_sb = -1;
         }
-        if (nx_sb >= 0) stage(Bn, ((int64_t)sbs_s[nx_sb] + nx_b) * 32);
-        float *const cst_s = cstb(B);
+        if (nx_sb >= 0) stage(nxt, cstn, ((int64_t)sbs_s[nx_sb] + nx_b) * 32);
+        const float *const cst_s = cstc;
         nproc++;
 
-        const __bf16 *hb = cbuf(B), *lb = hb + 32 * DP;
+        const __bf16 *hb = cur, *lb = hb + 32 * DP;
         // per-step LDS offsets recomputed each block (an opaque copy of the lane id keeps the
         // compiler from hoisting eight live address registers out of the loop: VGPR pressure)
         int colr = col;
@@ -840,7 +959,85 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
         bool hit = false;
 #pragma unroll
         for (int t = 0; t < QT; t++) hit |= m[t] >= a[t];
-        if (__ballot(hit)) {
+#if HDB_K1S_PROF
+        const uint64_t p_c = __builtin_readcyclecounter();
+        p_mfma += p_c - p_b;
+#endif
+        if (REG && __ballot(hit)) {
+#if HDB_K1S_PROF
+            p_hitsteps++;
+#endif
+            // both half-waves at once: each lane owns its (query, half) list and half-log
+            const double *c2d = (const double *)(cst_s + 64), *cnd = (const double *)(cst_s + 128);
+            unsigned mk = 0u;
+            if (m[0] >= a[0] && (qvm & 1u)) {
+#pragma unroll
+                for (int gi = 0; gi < 4; gi++) {
+                    const float4 h4 = hc4[2 * gi + half], c4 = cn4[2 * gi + half];
+                    mk |= (fmaf(g[0], c4.x, acc[0][4 * gi + 0]) - h4.x >= a[0]) ? 1u << (4 * gi + 0) : 0u;
+                    mk |= (fmaf(g[0], c4.y, acc[0][4 * gi + 1]) - h4.y >= a[0]) ? 1u << (4 * gi + 1) : 0u;
+                    mk |= (fmaf(g[0], c4.z, acc[0][4 * gi + 2]) - h4.z >= a[0]) ? 1u << (4 * gi + 2) : 0u;
+                    mk |= (fmaf(g[0], c4.w, acc[0][4 * gi + 3]) - h4.w >= a[0]) ? 1u << (4 * gi + 3) : 0u;
+                }
+            }
+            if (mk) {
+                int cq = col;
+                asm volatile("" : "+v"(cq));  // recomputed here: no loop-long address registers
+                const int ql = wave * 32 + cq;  // qloc_of(0) (QT = 1)
+                const int64_t qid = qbase + ql;
+                const double q2 = qn2_s[ql], qn = qn_s[ql];
+                int hh = half;
+                asm volatile("" : "+v"(hh));  // as cq: the half-log base is not hoisted (a 64-bit spill)
+                LogEnt *const L = logs + (qid * S_LOGCAP + hh * LH);
+                for (; mk; mk &= mk - 1) {
+                    const int r = __builtin_ctz(mk);
+                    const int ci = 8 * (r >> 2) + 4 * half + (r & 3);
+#if HDB_K1S_PROF
+                    p_hits++;
+#endif
+                    const float av = acc[0][r];  // dynamic element
+                    const int64_t cid = cb + ci;
+                    if ((ex && cid == qid) || cst_s[ci] == INFINITY) continue;  // self / padding row
+                    const double c2 = c2d[ci], cn = cnd[ci];
+                    const double approx = (q2 + c2) - 2.0 * (double)av;
+                    const double bound = eps_dot * qn * cn + 4e-13 * (q2 + c2) + 1e-30;
+                    const double lbv = approx - bound;
+                    const float thr = fminf(tl[KT], thq);
+                    if (!(lbv <= (double)thr)) continue;
+                    if (lcnt == LH) {
+                        lcnt = log_compact(L, thr, LH);
+                        if (lcnt == LH) {
+                            atomicAdd(overflow, 1);
+                            lcnt = LH + 1;  // this query's lists are not trusted
+                        }
+                    }
+                    if (lcnt < LH) {
+                        LogEnt e;
+                        e.cid = (int)cid;
+                        e.lb = f32_down(lbv);
+                        L[lcnt++] = e;
+                    }
+                    const float ub = f32_up(approx + bound);
+                    if (ub < tl[KT]) {  // insertion network (ascending)
+#pragma unroll
+                        for (int k = KT; k > 0; k--) tl[k] = ub < tl[k - 1] ? tl[k - 1] : fminf(tl[k], ub);
+                        tl[0] = fminf(tl[0], ub);
+                    }
+                }
+            }
+            thq = union_kth();
+            const float th = thq;
+            a[0] = qh[0] - 0.5f * th;
+            float wm = (qvm & 1u) ? th : -INFINITY;
+            for (int o = 32; o >= 1; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o));
+            wmax = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wm)));  // uniform
+#if HDB_K1S_PROF
+            p_hit += __builtin_readcyclecounter() - p_c;
+#endif
+        } else if (!REG && __ballot(hit)) {
+#if HDB_K1S_PROF
+            p_hitsteps++;
+#endif
             // rare: the two half-waves hold the same queries, so they take turns; each lane
             // walks only the set bits of its pass mask
             const double *c2d = (const double *)(cst_s + 64), *cnd = (const double *)(cst_s + 128);
@@ -870,9 +1067,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
                         for (unsigned mk = hm[t]; mk; mk &= mk - 1) {
                             const int r = __builtin_ctz(mk);
                             const int ci = 8 * (r >> 2) + 4 * half + (r & 3);
+#if HDB_K1S_PROF
+                            p_hits++;
+#endif
                             const float av = acc[t][r];  // dynamic element (rare path)
                             const int64_t cid = cb + ci;
-                            if ((ex && cid == qid) || sb.perm[cid] < 0) continue;
+                            // padding rows carry hc = +inf in the staged constants (an LDS read:
+                            // no dependent global load -- its vmcnt wait would also drain the
+                            // next block's LDS-DMA prefetch)
+                            if ((ex && cid == qid) || cst_s[ci] == INFINITY) continue;
                             const double c2 = c2d[ci], cn = cnd[ci];
                             const double approx = (q2 + c2) - 2.0 * (double)av;
                             const double bound = eps_dot * qn * cn + 4e-13 * (q2 + c2) + 1e-30;
@@ -915,6 +1118,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
             }
             for (int o = 32; o >= 1; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o));
             wmax = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wm)));  // uniform
+#if HDB_K1S_PROF
+            p_hit += __builtin_readcyclecounter() - p_c;
+#endif
         }
         if (lane == 0) tmax_s[par][wave] = wmax;
         par ^= 1;
@@ -931,7 +1137,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
         si_s[i] = (unsigned short)sb.sb_nblk[id];
     }
     __syncthreads();
-    stage(B0{}, (int64_t)sbs_s[0] * 32);
+#if HDB_K1S_PROF
+    p_setup = __builtin_readcyclecounter() - p_t0;
+#endif
+    auto step = [&](auto B, auto Bn) { body(cbuf(B), cbuf(Bn), cstb(B), cstb(Bn)); };
+    stage(cbuf(B0{}), cstb(B0{}), (int64_t)sbs_s[0] * 32);
     while (true) {
         step(B0{}, B1{});
         if (ci_sb < 0) break;
@@ -939,14 +1149,38 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
         if (ci_sb < 0) break;
     }
     if (sb.blocks_done && tid == 0) atomicAdd(sb.blocks_done, (unsigned long long)nproc);
+#if HDB_K1S_PROF
+    if (sb.blocks_done) {
+        if (lane == 0) {
+            atomicAdd(sb.blocks_done + 1, (unsigned long long)p_wait);
+            atomicAdd(sb.blocks_done + 2, (unsigned long long)p_mfma);
+            atomicAdd(sb.blocks_done + 3, (unsigned long long)p_hit);
+            atomicAdd(sb.blocks_done + 4, (unsigned long long)p_hitsteps);
+            atomicAdd(sb.blocks_done + 5, (unsigned long long)p_setup);
+            atomicAdd(sb.blocks_done + 6, (unsigned long long)nproc);
+        }
+        atomicAdd(sb.blocks_done + 7, (unsigned long long)p_hits);
+    }
+#endif
     __syncthreads();
-    for (int i = tid; i < SQ; i += 64 * NW) {
-        const int64_t qid = qbase + i;
-        if (sb.perm[qid] < 0) {
-            log_cnt[qid] = 0;
+    if constexpr (REG) {
+        const int64_t qid = qbase + qloc_of(0);
+        const float th = union_kth();
+        if (qvm & 1u) {
+            log_cnt[2 * qid + half] = lcnt > LH ? -1 : lcnt;
+            if (half == 0) thr_out[qid] = th;
         } else {
-            log_cnt[qid] = cnt_s[i] > S_LOGCAP ? -1 : cnt_s[i];
-            thr_out[qid] = top_s[i * KC + KC - 1];
+            log_cnt[2 * qid + half] = 0;
+        }
+    } else {
+        for (int i = tid; i < SQ; i += 64 * NW) {
+            const int64_t qid = qbase + i;
+            if (sb.perm[qid] < 0) {
+                log_cnt[qid] = 0;
+            } else {
+                log_cnt[qid] = cnt_s[i] > S_LOGCAP ? -1 : cnt_s[i];
+                thr_out[qid] = top_s[i * KC + KC - 1];
+            }
         }
     }
 }
@@ -990,7 +1224,9 @@ __global__ __launch_bounds__(256) void knn_mfma_final_kernel(const double *__res
     const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
 #endif
     if (q >= n || perm[q] < 0) return;  // n: layout rows here
-    const int cnt = log_cnt[q];
+    // REG screen: two half-logs of S_LOGCAP / 2 entries per query (the halves' counts at 2q, 2q+1)
+    constexpr bool REG = HDB_K1S_REGTOP && KC <= 15;
+    constexpr int NH = REG ? 2 : 1, LH = S_LOGCAP / NH;
     const float t = thr[q];
     const int64_t qo = perm[q];  // the query's row in X (the lists follow X's order)
     __shared__ double qrow_s[4][256];  // each wave's query row (d <= 256)
@@ -1007,25 +1243,31 @@ __global__ __launch_bounds__(256) void knn_mfma_final_kernel(const double *__res
     __shared__ int cl_s[4][S_LOGCAP];
     int *cl = cl_s[threadIdx.x >> 6];
     int np = 0;
-    for (int j0 = 0; j0 < cnt; j0 += 64) {
-        const int j = j0 + lane;
-        bool ok = false;
-        int cid = 0;
-        if (j < cnt) {
-            const LogEnt e = logs[q * S_LOGCAP + j];
-            ok = e.lb <= t;
-            cid = e.cid;
+    for (int h = 0; h < NH; h++) {
+        const int cnt = log_cnt[NH * q + h];
+        for (int j0 = 0; j0 < cnt; j0 += 64) {
+            const int j = j0 + lane;
+            bool ok = false;
+            int cid = 0;
+            if (j < cnt) {
+                const LogEnt e = logs[q * S_LOGCAP + h * LH + j];
+                ok = e.lb <= t;
+                cid = e.cid;
+            }
+            const unsigned long long m = __ballot(ok);
+            if (ok) cl[np + __popcll(m & ((1ull << lane) - 1))] = cid;
+            np += __popcll(m);
         }
-        const unsigned long long m = __ballot(ok);
-        if (ok) cl[np + __popcll(m & ((1ull << lane) - 1))] = cid;
-        np += __popcll(m);
     }
     __builtin_amdgcn_wave_barrier();
     for (int j = lane; j < np; j += 64) topk_insert<KC>(top, exact_sq_pf(qr, X + (int64_t)perm[cl[j]] * d, d));
 #else
-    for (int j = lane; j < cnt; j += 64) {
-        const LogEnt e = logs[q * S_LOGCAP + j];
-        if (e.lb <= t) topk_insert<KC>(top, exact_sq_pf(qr, X + (int64_t)perm[e.cid] * d, d));
+    for (int h = 0; h < NH; h++) {
+        const int cnt = log_cnt[NH * q + h];
+        for (int j = lane; j < cnt; j += 64) {
+            const LogEnt e = logs[q * S_LOGCAP + h * LH + j];
+            if (e.lb <= t) topk_insert<KC>(top, exact_sq_pf(qr, X + (int64_t)perm[e.cid] * d, d));
+        }
     }
 #endif
     for (int k = 0; k < KC; k++) {
@@ -1175,7 +1417,7 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
     double *prm = (double *)take(256);
     unsigned long long *stats = (unsigned long long *)take(256);
     float *cst = (float *)take(4 * (size_t)(n_cap / 32) * S_CST);
-    int *log_cnt = (int *)take(4 * (size_t)n_cap);
+    int *log_cnt = (int *)take(8 * (size_t)n_cap);  // per query, or per half-query (HDB_K1S_REGTOP)
     float *thr_f = (float *)take(4 * (size_t)n_cap);
     hipStream_t st = ctx->stream;
     hipLaunchKernelGGL(col_stats_kernel, dim3(nb), dim3(256), 0, st, X, n, d, nb, psum, pmax);
@@ -1275,8 +1517,18 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
             ctx->stats["knn_mfma_layout_rows"] = n_lay;
         }
         unsigned long long *blocks_done = stats + 1;
-        HIP_CHECK(hipMemsetAsync(blocks_done, 0, 8, st));
-        const SbArgs sbargs{qctr, qrn, sctr, srn, sb_blk_d, sb_nblk_d, perm, nsb, prune ? 1 : 0, blocks_done};
+        HIP_CHECK(hipMemsetAsync(blocks_done, 0, HDB_K1S_PROF ? 64 : 8, st));
+        float *sb_keys = nullptr;
+        if (prune && HDB_K1S_SBKEYS) {
+            int nsbp = 1;
+            while (nsbp < nsb) nsbp <<= 1;
+            const int64_t ngr = n_lp / Cf::SQ;
+            sb_keys = (float *)arena(ctx, A_SBKEY, 4 * (size_t)ngr * nsbp);
+            const double eps_dot = 2.0 * (3.1 * 0x1p-16 + 3.0 * DP * 0x1p-24) * 1.01;  // the screen's
+            hipLaunchKernelGGL(sb_keys_kernel<DP>, dim3((unsigned)ceil_div(nsbp, 64), (unsigned)ceil_div(ngr, (int64_t)16)),
+                               dim3(256), 0, st, qctr, qrn, sctr, srn, ngr, nsb, nsbp, eps_dot, sb_keys);
+        }
+        const SbArgs sbargs{qctr, qrn, sctr, srn, sb_blk_d, sb_nblk_d, perm, nsb, prune ? 1 : 0, blocks_done, sb_keys};
         {
             const int g = (int)std::min<int64_t>(ceil_div(n_lp, 256), 4096);
             hipLaunchKernelGGL(screen_consts_kernel, dim3(g), dim3(256), 0, st, nrm2, nrm, n_lp, perm, cst);
@@ -1299,18 +1551,23 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
         default: return false;
         }
 #undef K1S_CASE
-        unsigned long long h_st[2] = {0, 0};
-        HIP_CHECK(hipMemcpyAsync(h_st, stats, 16, hipMemcpyDeviceToHost, st));
+        unsigned long long h_st[9] = {};
+        HIP_CHECK(hipMemcpyAsync(h_st, stats, HDB_K1S_PROF ? 72 : 16, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
+        if (HDB_K1S_PROF) {  // summed over waves: cycles waiting, MFMA + screen, hit path; wave-steps
+            const char *nm[7] = {"wait", "mfma", "hit", "hitsteps", "setup", "wavesteps", "hits"};
+            for (int i = 0; i < 7; i++) ctx->stats[std::string("k1s_prof_") + nm[i]] = (int64_t)h_st[2 + i];
+        }
         const int h_ovf = (int)(h_st[0] & 0xffffffffull);
         ctx->stats["knn_mfma_blocks"] = (int64_t)h_st[1];  // (query group, 32-candidate block) pairs computed
         ctx->stats["knn_mfma_group_rows"] = Cf::SQ;
         if (ctx->count_evals) {
             // diagnostic: logged candidates (the FP64 re-checks are those with lb <= thr)
-            std::vector<int> hc((size_t)n_lp);
-            HIP_CHECK(hipMemcpy(hc.data(), log_cnt, 4 * (size_t)n_lp, hipMemcpyDeviceToHost));
+            const int nh = (HDB_K1S_REGTOP && KC <= 15) ? 2 : 1;
+            std::vector<int> hc((size_t)n_lp * nh);
+            HIP_CHECK(hipMemcpy(hc.data(), log_cnt, 4 * (size_t)n_lp * nh, hipMemcpyDeviceToHost));
             int64_t tot = 0;
-            for (int v : hc) tot += v < 0 ? S_LOGCAP : v;
+            for (int v : hc) tot += v < 0 ? S_LOGCAP / nh : v;
             ctx->stats["knn_mfma_rechecks"] = tot;
             ctx->stats["last_evals"] = tot;
         }

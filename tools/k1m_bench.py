@@ -50,6 +50,9 @@ if os.environ.get("K1M_QUICK"):
     out = {"n": n, "d": d, "lib": os.environ.get("HDBMI_LIB", "default"), "wall_s": dt, "knn_mfma_ms": ms,
            "knn_mfma_final_ms": ms_final, "knn_mfma_order_ms": ms_order, "blocks": nb,
            "block_frac": nb * rows * 32 / (n * n_pad)}
+    if os.environ.get("K1M_PROF"):  # a HDB_K1S_PROF=1 build: per-wave cycle split of the screen
+        for key in ("wait", "mfma", "hit", "hitsteps", "setup", "wavesteps", "hits"):
+            out["prof_" + key] = ctx.get_stat("k1s_prof_" + key)
     if os.environ.get("K1M_DIAG"):
         ctx.set_option("count_evals", 1)
         star.knn(X, k, None, exclSelf=True)
