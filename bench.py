@@ -135,7 +135,9 @@ MFMA_BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
 PMC_C2 = next((p for p in (os.path.join(ROOT, "profiles", r, "final", "prof_c2", "pmc_summary.json")
                             for r in ("r03", "r02")) if os.path.exists(p)),
               os.path.join(ROOT, "profiles", "r02", "final", "prof_c2", "pmc_summary.json"))
-PMC_C4 = os.path.join(ROOT, "profiles", "r02", "c4_final", "pmc_summary.json")
+PMC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, "c4_final", "pmc_summary.json")
+                            for r in ("r03", "r02")) if os.path.exists(p)),
+              os.path.join(ROOT, "profiles", "r02", "c4_final", "pmc_summary.json"))
 
 
 def _pmc_bytes(path, kernel):
