@@ -487,6 +487,8 @@ def main():
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process group for N>1 (gloo: rehearse several ranks on one device)")
     ap.add_argument("--phases", action="store_true", help="c3/c5: per-phase times (synchronising)")
+    ap.add_argument("--mst-workers", type=int, default=int(os.environ.get("HDB_BENCH_MST_WORKERS", "1")),
+                    help="c2: partitions in flight in stage 1 (one thread, context and stream each)")
     args = ap.parse_args()
     if args.steps is None:
         args.steps = {"c2": 10, "c4": 5}.get(args.workload, 1)
@@ -621,6 +623,70 @@ def main():
             self.q.put(None)
             self.t.join()
 
+    class MstWorkers:
+        """Stage 1 on M threads (own library context and HIP stream each): partition i's exact
+        MST (K1t cores -> K2b Boruvka + self edges) and its sort run on worker i % M, so one
+        partition's latency-bound Boruvka rounds overlap the next partition's k-NN.  Results
+        are taken in step order; the N>1 gather (a collective) stays on the main thread, in step
+        order on every rank."""
+
+        def __init__(self, m):
+            self.m = m
+            self.qs = [queue.Queue() for _ in range(m)]
+            self.res = {}
+            self.cv = threading.Condition()
+            self.ctxs = [None] * m
+            self.ready = threading.Barrier(m + 1)
+            self.ts = [threading.Thread(target=self._run, args=(j,), daemon=True) for j in range(m)]
+            for t in self.ts:
+                t.start()
+            self.ready.wait()
+
+        def _run(self, j):
+            torch.cuda.set_device(local)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                c = pkg.Context.get(local)  # thread-local: this worker's own context
+                c.use_torch_stream()
+                st = pkg.HDBSCANStar(c)
+                self.ctxs[j] = c
+                self.ready.wait()
+                while True:
+                    i = self.qs[j].get()
+                    if i is None:
+                        return
+                    try:
+                        _, mst = st.exactMST(X_res, MIN_PTS, None, pkg.CORE_EXCL_SELF, True)
+                        own = pkg.sort_edges_desc(mst.getVerticeA(), mst.getVericeB(), mst.getEges(), c)
+                        ev = torch.cuda.Event()
+                        ev.record()
+                        out = (ev, own)
+                    except BaseException as e:  # re-raised on the main thread
+                        out = e
+                    with self.cv:
+                        self.res[i] = out
+                        self.cv.notify_all()
+
+        def submit(self, i):
+            self.qs[i % self.m].put(i)
+
+        def result(self, i):
+            with self.cv:
+                self.cv.wait_for(lambda: i in self.res)
+                out = self.res.pop(i)
+            if isinstance(out, BaseException):
+                raise out
+            return out
+
+        def close(self):
+            for q in self.qs:
+                q.put(None)
+            for t in self.ts:
+                t.join()
+
+    M = max(1, args.mst_workers)
+    workers = MstWorkers(M) if M > 1 else None
+
     stage = LabelStage()
     # H2D of step i+1's points on a copy stream during step i's MST (two point buffers)
     X_bufs = [X_dev, torch.empty_like(X_dev)]
@@ -640,6 +706,19 @@ def main():
         resident: the points are already in HBM (no H2D: the value's timed region);
         otherwise every step uploads its points from pinned host memory first"""
         i0 = pipe["next"]
+        if resident and workers is not None:  # M partitions in flight in stage 1
+            for i in range(i0, min(i0 + M, i0 + steps)):
+                workers.submit(i)
+            for i in range(i0, i0 + steps):
+                ev, own = workers.result(i)
+                if i + M < i0 + steps:
+                    workers.submit(i + M)
+                torch.cuda.current_stream().wait_event(ev)
+                merged = par.gather_sorted_msts(*own, dst=0) if world > 1 else own
+                stage.submit(own, merged if rank == 0 else None)
+            pipe["next"] = i0 + steps
+            stage.drain()
+            return
         if not resident:
             prefetch(i0)
         for i in range(i0, i0 + steps):
@@ -672,19 +751,24 @@ def main():
     # per-kernel device times: HIP events recorded on the launch streams inside the timed
     # region (measured cost of the records: ~1% of a step)
     keys = ("knn_tree", "boruvka_total", "boruvka_scan", "merge_sort")
-    for c in (ctx, stage.ctx):
+    s1 = workers.ctxs if workers is not None else [ctx]  # stage-1 contexts
+    for c in (*s1, stage.ctx):
         c.set_timing(True)
     for k in keys:
-        ctx.kernel_time(k)
+        for c in s1:
+            c.kernel_time(k)
     stage.ctx.kernel_time("flat_labels")
     barrier()
     t0 = time.perf_counter()
     pipe_run(args.steps, resident=True)
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
-    for c in (ctx, stage.ctx):
+    for c in (*s1, stage.ctx):
         c.set_timing(False)
-    kt = {k: ctx.kernel_time(k) for k in keys}
+    kt = {}
+    for k in keys:
+        tm = [c.kernel_time(k) for c in s1]
+        kt[k] = (sum(t[0] for t in tm), sum(t[1] for t in tm))
     kt["flat_labels"] = stage.ctx.kernel_time("flat_labels")
     # the same pipeline with every step's points uploaded from pinned host memory
     # (PCIe-inclusive; reported beside the value, never as it)
@@ -694,6 +778,8 @@ def main():
     barrier()
     dt_pcie = max_over_ranks(time.perf_counter() - t0)
     stage.close()
+    if workers is not None:
+        workers.close()
     # latency of one step without the pipeline (each step's stages back to back)
     step_e2e()
     barrier()
@@ -782,6 +868,7 @@ def main():
                    "stream) -> D2H of the labels; pipelined: step i's labels + D2H (own thread, stream and "
                    "library context) overlap step i+1's MST + merge; the timer stops after the last step's "
                    "labels are on the host",
+                   "stage1_partitions_in_flight": M,
                    "parallelism": f"partition-sharded x{world}"},
         "n_clusters": n_clusters[0],
         "pcie_inclusive_points_per_s": total_points * tsteps / dt_pcie,
