@@ -489,6 +489,8 @@ def main():
     ap.add_argument("--phases", action="store_true", help="c3/c5: per-phase times (synchronising)")
     ap.add_argument("--mst-workers", type=int, default=int(os.environ.get("HDB_BENCH_MST_WORKERS", "1")),
                     help="c2: partitions in flight in stage 1 (one thread, context and stream each)")
+    ap.add_argument("--label-workers", type=int, default=int(os.environ.get("HDB_BENCH_LABEL_WORKERS", "0")),
+                    help="c2: label stages (0: as many as --mst-workers)")
     args = ap.parse_args()
     if args.steps is None:
         args.steps = {"c2": 10, "c4": 5}.get(args.workload, 1)
@@ -566,7 +568,8 @@ def main():
         the GIL).  Every step still does all of its work; the timer stops after the last
         step's stage 2 has finished."""
 
-        def __init__(self):
+        def __init__(self, bufs):
+            self.bufs = bufs  # this stage's pinned host buffers (merged va, vb, w; labels)
             self.q = queue.Queue(maxsize=1)
             self.err = None
             self.ready = threading.Event()
@@ -593,11 +596,11 @@ def main():
                         if merged is not None:  # rank 0: D2H of the merged list beside the labels
                             cs.wait_event(ev)
                             with torch.cuda.stream(cs):
-                                va_h.copy_(merged[0], non_blocking=True)
-                                vb_h.copy_(merged[1], non_blocking=True)
-                                w_h.copy_(merged[2], non_blocking=True)
+                                self.bufs[0].copy_(merged[0], non_blocking=True)
+                                self.bufs[1].copy_(merged[1], non_blocking=True)
+                                self.bufs[2].copy_(merged[2], non_blocking=True)
                         lab, k = pkg.flat_labels(*own, n, MIN_CL_SIZE, ctx=self.ctx)
-                        lab_h.copy_(lab, non_blocking=True)
+                        self.bufs[3].copy_(lab, non_blocking=True)
                         s.synchronize()
                         cs.synchronize()
                         n_clusters[0] = k
@@ -687,7 +690,33 @@ def main():
     M = max(1, args.mst_workers)
     workers = MstWorkers(M) if M > 1 else None
 
-    stage = LabelStage()
+    class LabelStages:
+        """L label stages (one thread, context and stream each), steps dealt round-robin: with
+        several partitions in flight in stage 1 one label stage becomes the bottleneck.  Stage
+        0 writes the host buffers the final checks read; the others have their own."""
+
+        def __init__(self, nl):
+            pin = lambda t: t.pin_memory()
+            self.st = [LabelStage((va_h, vb_h, w_h, lab_h) if j == 0 else
+                                  (pin(torch.empty_like(va_h)), pin(torch.empty_like(vb_h)),
+                                   pin(torch.empty_like(w_h)), pin(torch.empty_like(lab_h)))) for j in range(nl)]
+            self.ctxs = [x.ctx for x in self.st]
+            self.k = 0
+
+        def submit(self, own, merged):
+            self.st[self.k % len(self.st)].submit(own, merged)
+            self.k += 1
+
+        def drain(self):
+            for x in self.st:
+                x.drain()
+
+        def close(self):
+            for x in self.st:
+                x.close()
+
+    L = max(1, args.label_workers if args.label_workers else M)
+    stage = LabelStages(L)
     # H2D of step i+1's points on a copy stream during step i's MST (two point buffers)
     X_bufs = [X_dev, torch.empty_like(X_dev)]
     h2d_s = torch.cuda.Stream()
@@ -752,24 +781,26 @@ def main():
     # region (measured cost of the records: ~1% of a step)
     keys = ("knn_tree", "boruvka_total", "boruvka_scan", "merge_sort")
     s1 = workers.ctxs if workers is not None else [ctx]  # stage-1 contexts
-    for c in (*s1, stage.ctx):
+    for c in (*s1, *stage.ctxs):
         c.set_timing(True)
     for k in keys:
         for c in s1:
             c.kernel_time(k)
-    stage.ctx.kernel_time("flat_labels")
+    for c in stage.ctxs:
+        c.kernel_time("flat_labels")
     barrier()
     t0 = time.perf_counter()
     pipe_run(args.steps, resident=True)
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
-    for c in (*s1, stage.ctx):
+    for c in (*s1, *stage.ctxs):
         c.set_timing(False)
     kt = {}
     for k in keys:
         tm = [c.kernel_time(k) for c in s1]
         kt[k] = (sum(t[0] for t in tm), sum(t[1] for t in tm))
-    kt["flat_labels"] = stage.ctx.kernel_time("flat_labels")
+    tl = [c.kernel_time("flat_labels") for c in stage.ctxs]
+    kt["flat_labels"] = (sum(t[0] for t in tl), sum(t[1] for t in tl))
     # the same pipeline with every step's points uploaded from pinned host memory
     # (PCIe-inclusive; reported beside the value, never as it)
     barrier()
@@ -868,7 +899,7 @@ def main():
                    "stream) -> D2H of the labels; pipelined: step i's labels + D2H (own thread, stream and "
                    "library context) overlap step i+1's MST + merge; the timer stops after the last step's "
                    "labels are on the host",
-                   "stage1_partitions_in_flight": M,
+                   "stage1_partitions_in_flight": M, "label_stages": L,
                    "parallelism": f"partition-sharded x{world}"},
         "n_clusters": n_clusters[0],
         "pcie_inclusive_points_per_s": total_points * tsteps / dt_pcie,
