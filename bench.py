@@ -12,6 +12,11 @@ every rank owns its own 1M-point partition (weak scaling, as MR-HDBSCAN* shards 
 each rank labels its partition, and the merge all-gathers every rank's edge list over RCCL
 before the sort (rank 0 copies the merged list out).
 
+Several partitions are in flight on one GPU (MR-HDBSCAN* maps over independent partitions):
+--mst-workers stage-1 threads (exact MST + sort, own context and stream each; default 3) and
+--label-workers label stages (default 2), so one partition's latency-bound Boruvka rounds and
+flat-label kernels overlap the next partitions' work.  Every step still does all of its work.
+
 Prints ONE JSON line (rank 0).  value = points/s over all ranks, end to end from points
 already resident in HBM (the labels and the merged list still come back to host memory);
 pcie_inclusive_points_per_s = the same pipeline with every step's points uploaded from pinned
@@ -487,9 +492,9 @@ def main():
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process group for N>1 (gloo: rehearse several ranks on one device)")
     ap.add_argument("--phases", action="store_true", help="c3/c5: per-phase times (synchronising)")
-    ap.add_argument("--mst-workers", type=int, default=int(os.environ.get("HDB_BENCH_MST_WORKERS", "1")),
+    ap.add_argument("--mst-workers", type=int, default=int(os.environ.get("HDB_BENCH_MST_WORKERS", "3")),
                     help="c2: partitions in flight in stage 1 (one thread, context and stream each)")
-    ap.add_argument("--label-workers", type=int, default=int(os.environ.get("HDB_BENCH_LABEL_WORKERS", "0")),
+    ap.add_argument("--label-workers", type=int, default=int(os.environ.get("HDB_BENCH_LABEL_WORKERS", "2")),
                     help="c2: label stages (0: as many as --mst-workers)")
     args = ap.parse_args()
     if args.steps is None:
