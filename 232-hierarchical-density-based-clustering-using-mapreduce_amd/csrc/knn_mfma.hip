@@ -396,7 +396,8 @@ __device__ __forceinline__ int64_t xcd_contig(int64_t b, int64_t G) {
     return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
 }
 #ifndef HDB_K1S_WPE
-#define HDB_K1S_WPE (HDB_K1S_QT == 1 ? (HDB_K1S_REGTOP ? 3 : 4) : 2)
+#define HDB_K1S_WPE (HDB_K1S_QT == 1 ? (HDB_K1S_REGTOP ? 2 : 4) : 2)  // REGTOP: one 8-wave workgroup per CU
+                                                                      // either way; 2 leaves 192 VGPRs (A/B: 37.5 -> 36.9 ms)
 #endif
 constexpr int K1S_WPE = HDB_K1S_WPE;  // waves per SIMD (A/B at C4: 4 = two workgroups per CU, 51.7 ms, despite
                                       // spilling some fragments; 3 = 168 VGPRs without spills, one workgroup, 57.0 ms)
