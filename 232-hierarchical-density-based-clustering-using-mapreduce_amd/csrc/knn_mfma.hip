@@ -385,6 +385,9 @@ constexpr int NW = HDB_K1S_WAVES;
 #ifndef HDB_K1F_COMPACT
 #define HDB_K1F_COMPACT 1  // re-check: compact the surviving log entries first (A/B at C4: 23.6 -> 16.3 ms)
 #endif
+#ifndef HDB_K1F_QPW
+#define HDB_K1F_QPW 1  // re-check: queries per wave (4: knn_mfma_final16_kernel, 16 lanes each; 1: a wave each)
+#endif
 #ifndef HDB_K1F_XCD
 #define HDB_K1F_XCD 0  // the same for the re-check's query blocks
 #endif
@@ -1371,6 +1374,84 @@ __global__ __launch_bounds__(256) void knn_mfma_final_kernel(const double *__res
     }
 }
 
+// The same re-check with 16 lanes per query, four queries per wave: a query keeps ~KC
+// survivors, so a wave per query left most lanes idle while its few lanes streamed 1 KB rows
+// at HBM latency.  Per 16-lane group: the surviving log entries (lb <= thr) are compacted into
+// LDS 256 at a time, every lane computes the exact FP64 distances of its survivors in the
+// reference's order (one lane per candidate: the sequential sum is the bit-exact one), and the
+// KC smallest come out of a 16-lane min/ballot selection.  Query rows in dynamic LDS (16 x d).
+constexpr int K1F_CH = 256;  // compacted survivors per group and pass
+template <int KC>
+__global__ __launch_bounds__(256) void knn_mfma_final16_kernel(const double *__restrict__ X, int64_t n, int d,
+                                                               const LogEnt *__restrict__ logs,
+                                                               const int *__restrict__ log_cnt,
+                                                               const float *__restrict__ thr,
+                                                               const int *__restrict__ perm,
+                                                               double *__restrict__ lists) {
+    constexpr bool REG = HDB_K1S_REGTOP && KC <= 15;
+    constexpr int NH = REG ? 2 : 1, LH = S_LOGCAP / NH;
+    extern __shared__ __attribute__((aligned(16))) double k1f_dyn[];
+    __shared__ int cl_s[16][K1F_CH];
+    const int lane = threadIdx.x & 63, sub = lane >> 4, sl = lane & 15;
+    const int g = (threadIdx.x >> 6) * 4 + sub;  // query slot in the workgroup
+    const int64_t q = (int64_t)blockIdx.x * 16 + g;
+    const bool act = q < n && perm[q] >= 0;  // n: layout rows here (uniform per 16 lanes)
+    double *qr = k1f_dyn + (size_t)g * d;
+    const int64_t qo = act ? perm[q] : 0;  // the query's row in X (the lists follow X's order)
+    if (act)
+        for (int c = sl; c < d; c += 16) qr[c] = X[qo * d + c];
+    const float t = act ? thr[q] : 0.f;
+    double top[KC];
+#pragma unroll
+    for (int k = 0; k < KC; k++) top[k] = INFINITY;
+    const unsigned long long below = (1ull << lane) - 1;
+    int *cl = cl_s[g];
+    for (int h = 0; h < NH; h++) {
+        const int cnt = act ? log_cnt[NH * q + h] : 0;
+        const LogEnt *L = logs + q * S_LOGCAP + h * LH;
+        for (int j0 = 0; j0 < LH; j0 += K1F_CH) {
+            // compaction of entries [j0, j0 + K1F_CH) of this half-log
+            int np = 0;
+            for (int j1 = j0; j1 < j0 + K1F_CH; j1 += 64) {
+                LogEnt e[4];
+                bool ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {  // four loads in flight per lane
+                    const int j = j1 + 16 * u + sl;
+                    ok[u] = j < cnt;
+                    if (ok[u]) e[u] = L[j];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const bool sv = ok[u] && e[u].lb <= t;
+                    const unsigned long long m = __ballot(sv);
+                    const unsigned long long mg = (m >> (16 * sub)) & 0xFFFFull;
+                    if (sv) cl[np + __popcll(m & below & (0xFFFFull << (16 * sub)))] = e[u].cid;
+                    np += __popcll(mg);
+                }
+                if (!__ballot(j1 + 64 < cnt)) break;  // wave-uniform: the rest of the pass is empty
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int j = sl; j < np; j += 16) topk_insert<KC>(top, exact_sq_pf(qr, X + (int64_t)perm[cl[j]] * d, d));
+            __builtin_amdgcn_wave_barrier();
+            if (!__ballot(j0 + K1F_CH < cnt)) break;  // wave-uniform: no group has more entries
+        }
+    }
+    // the KC smallest over the 16 lanes of the group
+    for (int k = 0; k < KC; k++) {
+        double mn = top[0];
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
+        const unsigned long long b = (__ballot(top[0] == mn) >> (16 * sub)) & 0xFFFFull;
+        if (sl == __ffsll((long long)b) - 1) {
+#pragma unroll
+            for (int i = 0; i + 1 < KC; i++) top[i] = top[i + 1];
+            top[KC - 1] = INFINITY;
+        }
+        if (act && sl == 0) lists[qo * KC + k] = (mn < INFINITY) ? sqrt(mn) : JMAX;
+    }
+}
+
 // ---------------------------------------------------------------- host
 template <int DP, int KC>
 static void launch_single(hdb_ctx *ctx, const double *X, int64_t n, int64_t n_pad, int d, const __bf16 *Xh,
@@ -1387,8 +1468,12 @@ static void launch_single(hdb_ctx *ctx, const double *X, int64_t n, int64_t n_pa
     }
     {
         KernelTimer t(ctx, "knn_mfma_final");
-        hipLaunchKernelGGL((knn_mfma_final_kernel<KC>), dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, X, n, d,
-                           logs, log_cnt, thr, perm, lists);
+        if (HDB_K1F_QPW == 4)
+            hipLaunchKernelGGL((knn_mfma_final16_kernel<KC>), dim3((unsigned)ceil_div(n, 16)), dim3(256),
+                               (unsigned)(16 * 8 * d), st, X, n, d, logs, log_cnt, thr, perm, lists);
+        else
+            hipLaunchKernelGGL((knn_mfma_final_kernel<KC>), dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, X, n,
+                               d, logs, log_cnt, thr, perm, lists);
         HIP_CHECK(hipGetLastError());
     }
 }
