@@ -41,7 +41,7 @@ namespace hdb {
 namespace {
 
 constexpr int32_t NONE = INT32_MAX;
-enum : int { FE_RANGE = 1, FE_NAN = 2, FE_CYCLE = 4, FE_ISOLATED = 8, FE_ROOTS = 16 };
+enum : int { FE_RANGE = 1, FE_NAN = 2, FE_CYCLE = 4, FE_ISOLATED = 8, FE_ROOTS = 16, FE_JUMP = 32 };
 
 // ------------------------------------------------------------------------- union-find
 // Randomised linking: the root with the lower (priority, id) hooks under the higher one, so
@@ -736,6 +736,14 @@ __global__ void fl_jump(int32_t *__restrict__ up, int64_t m, const int *__restri
         }
     }
     flag_or(flag_next, ch);
+}
+
+// the launch counts below are sized from the reach a launch guarantees when every read
+// returns the value from the start of the launch (the writer may sit on another XCD): 5x for
+// fl_jump's two 2-hop steps, 4x for three doublings; one launch more than convergence needs,
+// so its flag is zero unless a chain outran the bound -- then the result is not trusted
+__global__ void fl_jump_check(const int *__restrict__ flag_last, int *__restrict__ err) {
+    if (threadIdx.x == 0 && *flag_last != 0) atomicOr(err, FE_JUMP);
 }
 
 struct NodeArr {
@@ -1526,14 +1534,16 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     unsigned long long *hkey = (unsigned long long *)(pwide + 2 * m);
     int *ffl = (int *)(hkey + m);  // 192 jump flags
     int32_t *mk = cv2.take<int32_t>(n), *rk = cv2.take<int32_t>(n);
+    // guaranteed reach 5x per fl_jump launch (see fl_jump_check): ceil(log5 m) launches + one
     int rounds = 2;
-    for (int64_t span = 9; span < m; span *= 9) rounds++;
+    for (int64_t span = 5; span < m; span *= 5) rounds++;
     rounds = std::min(rounds, 64);
     auto jump_all = [&](int32_t *up) {  // roots of an upward forest, in place
         HIP_CHECK(hipMemsetAsync(jflags, 0, sizeof(int) * 64, st));
         for (int k = 0; k < rounds; k++)
             hipLaunchKernelGGL(fl_jump, dim3(g / 4 + 1), dim3(1024), 0, st, up, m, k ? jflags + k - 1 : nullptr,
                                jflags + k);
+        hipLaunchKernelGGL(fl_jump_check, dim3(1), dim3(64), 0, st, jflags + rounds - 1, err);
     };
 
     hipLaunchKernelGGL(fl_tie_up, dim3(g), dim3(256), 0, st, dc.parent, ew, m, top, err);
@@ -1572,12 +1582,15 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     hipLaunchKernelGGL(fl_stab, dim3((int)std::min<int64_t>(m, 16384)), dim3(64), 0, st, val2, seg, seg_hi, Kp, stab, err);
 
     // ---- 5. FOSC on the device (heavy-path walkers), selection, labels
-    int jrounds = 2;  // three doublings per launch: 8x reach per launch
-    for (int64_t reach = 1; reach < m; reach *= 8) jrounds++;
+    // three doublings per launch: guaranteed reach 4x per launch under stale reads (8x when the
+    // reads see this launch's writes); ceil(log4 m) launches + one, checked
+    int jrounds = 2;
+    for (int64_t span = 4; span < m; span *= 4) jrounds++;
     jrounds = std::min(jrounds, 64);
     auto jump64 = [&](auto kern, uint64_t *wd, int *flags) {  // flags: jrounds ints, zeroed below
         for (int k = 0; k < jrounds; k++)
             hipLaunchKernelGGL(kern, dim3(g / 4 + 1), dim3(1024), 0, st, wd, Kp, k ? flags + k - 1 : nullptr, flags + k, err);
+        hipLaunchKernelGGL(fl_jump_check, dim3(1), dim3(64), 0, st, flags + jrounds - 1, err);
     };
     // zero: nch, kcur, plen, maxld, hkey (contiguous) and the jump flags
     HIP_CHECK(hipMemsetAsync(fz, 0, fz_bytes, st));
@@ -1634,6 +1647,7 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     const int e1 = (int)pin[1];
     if (e1 & FE_CYCLE) HDB_THROW(HDB_EINVAL, "flat labels: the edges contain a cycle");
     if (e1 & FE_ROOTS) HDB_THROW(HDB_EINVAL, "flat labels: the edges are not a spanning tree");
+    if (e1 & FE_JUMP) HDB_THROW(HDB_EDEVICE, "flat labels: pointer jumping did not converge in its launch budget");
     if (n_clusters) *n_clusters = pin[3];
     ctx->stats["flat_clusters_total"] = *(int32_t *)(pin + 4);  // condensed-tree clusters incl. the root
 }

@@ -382,15 +382,6 @@ constexpr int NW = HDB_K1S_WAVES;
 #ifndef HDB_K1S_PROF
 #define HDB_K1S_PROF 0  // diagnostic build: per-wave cycle split of the screen loop (stats k1s_prof_*)
 #endif
-#ifndef HDB_K1F_COMPACT
-#define HDB_K1F_COMPACT 1  // re-check: compact the surviving log entries first (A/B at C4: 23.6 -> 16.3 ms)
-#endif
-#ifndef HDB_K1F_QPW
-#define HDB_K1F_QPW 1  // re-check: queries per wave (4: knn_mfma_final16_kernel, 16 lanes each; 1: a wave each)
-#endif
-#ifndef HDB_K1F_XCD
-#define HDB_K1F_XCD 0  // the same for the re-check's query blocks
-#endif
 #define K1S_XCD HDB_K1S_XCD
 // Workgroups are dealt round-robin over the 8 XCDs (block b runs on XCD b mod 8); this maps
 // them so XCD x takes one contiguous range of logical blocks (a bijection on [0, G)).
@@ -1301,81 +1292,8 @@ __device__ __forceinline__ double exact_sq_pf(const double *a_lds, const double 
     return sx;
 }
 
-template <int KC>
-__global__ __launch_bounds__(256) void knn_mfma_final_kernel(const double *__restrict__ X, int64_t n, int d,
-                                                             const LogEnt *__restrict__ logs,
-                                                             const int *__restrict__ log_cnt,
-                                                             const float *__restrict__ thr,
-                                                             const int *__restrict__ perm,
-                                                             double *__restrict__ lists) {
-    const int lane = threadIdx.x & 63;
-#if HDB_K1F_XCD
-    const int64_t q = ((xcd_contig(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) >> 6);
-#else
-    const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-#endif
-    if (q >= n || perm[q] < 0) return;  // n: layout rows here
-    // REG screen: two half-logs of S_LOGCAP / 2 entries per query (the halves' counts at 2q, 2q+1)
-    constexpr bool REG = HDB_K1S_REGTOP && KC <= 15;
-    constexpr int NH = REG ? 2 : 1, LH = S_LOGCAP / NH;
-    const float t = thr[q];
-    const int64_t qo = perm[q];  // the query's row in X (the lists follow X's order)
-    __shared__ double qrow_s[4][256];  // each wave's query row (d <= 256)
-    double *qr = qrow_s[threadIdx.x >> 6];
-    for (int c = lane; c < d; c += 64) qr[c] = X[qo * d + c];
-    double top[KC];
-#pragma unroll
-    for (int k = 0; k < KC; k++) top[k] = INFINITY;
-#if HDB_K1F_COMPACT
-    // the entries that survive the final threshold are compacted first (ballot + prefix into
-    // LDS), so every lane streams a candidate row in each pass instead of idling on the
-    // entries lb > thr filters out; the KC smallest over the wave do not depend on which lane
-    // evaluated which candidate
-    __shared__ int cl_s[4][S_LOGCAP];
-    int *cl = cl_s[threadIdx.x >> 6];
-    int np = 0;
-    for (int h = 0; h < NH; h++) {
-        const int cnt = log_cnt[NH * q + h];
-        for (int j0 = 0; j0 < cnt; j0 += 64) {
-            const int j = j0 + lane;
-            bool ok = false;
-            int cid = 0;
-            if (j < cnt) {
-                const LogEnt e = logs[q * S_LOGCAP + h * LH + j];
-                ok = e.lb <= t;
-                cid = e.cid;
-            }
-            const unsigned long long m = __ballot(ok);
-            if (ok) cl[np + __popcll(m & ((1ull << lane) - 1))] = cid;
-            np += __popcll(m);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (int j = lane; j < np; j += 64) topk_insert<KC>(top, exact_sq_pf(qr, X + (int64_t)perm[cl[j]] * d, d));
-#else
-    for (int h = 0; h < NH; h++) {
-        const int cnt = log_cnt[NH * q + h];
-        for (int j = lane; j < cnt; j += 64) {
-            const LogEnt e = logs[q * S_LOGCAP + h * LH + j];
-            if (e.lb <= t) topk_insert<KC>(top, exact_sq_pf(qr, X + (int64_t)perm[e.cid] * d, d));
-        }
-    }
-#endif
-    for (int k = 0; k < KC; k++) {
-        double mn = top[0];
-        for (int o = 32; o >= 1; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
-        const unsigned long long b = __ballot(top[0] == mn);
-        if (lane == __ffsll((long long)b) - 1) {
-#pragma unroll
-            for (int i = 0; i + 1 < KC; i++) top[i] = top[i + 1];
-            top[KC - 1] = INFINITY;
-        }
-        if (lane == 0) lists[qo * KC + k] = (mn < INFINITY) ? sqrt(mn) : JMAX;
-    }
-}
-
-// The same re-check with 16 lanes per query, four queries per wave: a query keeps ~KC
-// survivors, so a wave per query left most lanes idle while its few lanes streamed 1 KB rows
+// The exact FP64 re-check, 16 lanes per query, four queries per wave: a query keeps ~KC
+// survivors, so a wave per query (round 3's kernel, 17.4 ms at C4; this one 15.6 ms) left most lanes idle while its few lanes streamed 1 KB rows
 // at HBM latency.  Per 16-lane group: the surviving log entries (lb <= thr) are compacted into
 // LDS 256 at a time, every lane computes the exact FP64 distances of its survivors in the
 // reference's order (one lane per candidate: the sequential sum is the bit-exact one), and the
@@ -1468,12 +1386,8 @@ static void launch_single(hdb_ctx *ctx, const double *X, int64_t n, int64_t n_pa
     }
     {
         KernelTimer t(ctx, "knn_mfma_final");
-        if (HDB_K1F_QPW == 4)
-            hipLaunchKernelGGL((knn_mfma_final16_kernel<KC>), dim3((unsigned)ceil_div(n, 16)), dim3(256),
-                               (unsigned)(16 * 8 * d), st, X, n, d, logs, log_cnt, thr, perm, lists);
-        else
-            hipLaunchKernelGGL((knn_mfma_final_kernel<KC>), dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, X, n,
-                               d, logs, log_cnt, thr, perm, lists);
+        hipLaunchKernelGGL((knn_mfma_final16_kernel<KC>), dim3((unsigned)ceil_div(n, 16)), dim3(256),
+                           (unsigned)(16 * 8 * d), st, X, n, d, logs, log_cnt, thr, perm, lists);
         HIP_CHECK(hipGetLastError());
     }
 }

@@ -17,10 +17,10 @@ Several partitions are in flight on one GPU (MR-HDBSCAN* maps over independent p
 --label-workers label stages (default 2), so one partition's latency-bound Boruvka rounds and
 flat-label kernels overlap the next partitions' work.  Every step still does all of its work.
 
-Prints ONE JSON line (rank 0).  value = points/s over all ranks, end to end from points
-already resident in HBM (the labels and the merged list still come back to host memory);
-pcie_inclusive_points_per_s = the same pipeline with every step's points uploaded from pinned
-host memory first; device_resident_points_per_s = MST + merge only (HBM to HBM, no labels).
+Prints ONE JSON line (rank 0).  value = points/s over all ranks, end to end from parsed points
+in pinned host memory (every step uploads its points inside the timed region) to the merged
+list and labels back in host memory; hbm_resident_points_per_s = the same pipeline from points
+already in HBM; device_resident_points_per_s = MST + merge only (HBM to HBM, no labels).
 """
 from __future__ import annotations
 
@@ -156,9 +156,9 @@ def run_c4(args):
     """BASELINE config 4: 2M x 128 L2-normalised embeddings, core distances over minPts = 16
     (EXCL_SELF) on the MFMA path (K1m: k-means layout, bf16-split norm-expansion screen on MFMA
     over the (query group, candidate block) pairs the FP64 balls cannot exclude, candidate log,
-    exact FP64 re-check of the log; lists bit-identical to the FP64 scan).  Timed region: X
-    resident in HBM -> core distances -> D2H of the cores (the PCIe-inclusive rate from pinned
-    host memory rides along).  One GPU (the core distances of one
+    exact FP64 re-check of the log; lists bit-identical to the FP64 scan).  Timed region: X in
+    pinned host memory -> H2D -> core distances -> D2H of the cores (the HBM-resident rate rides
+    along).  One GPU (the core distances of one
     partition; C4 names no sharding).  Roofline of the screen kernel: the MFMA flops it issues
     (3 bf16 products per pair of every computed block pair) / its time vs the dense bf16 peak;
     the all-pairs-equivalent 2 n^2 d rate rides along."""
@@ -173,40 +173,62 @@ def run_c4(args):
     X = C[lab] + C4["noise"] * torch.randn(n, d, dtype=torch.float64, device="cuda", generator=g)
     X_pin = (X / torch.linalg.norm(X, dim=1, keepdim=True)).cpu().pin_memory()
     del X, C, lab
+    torch.cuda.empty_cache()
     ctx = pkg.Context.get(0)
     ctx.use_torch_stream()
     core_h = torch.empty(n, dtype=torch.float64).pin_memory()
     X_res = X_pin.cuda()  # the input resident in HBM (the value's timed region starts there)
 
-    def step(resident=True):
-        Xd = X_res if resident else X_pin.to("cuda", non_blocking=True)
-        core = torch.empty(n, dtype=torch.float64, device="cuda")
-        A.check(A.lib().hdb_core_distances(ctx.h, Xd.data_ptr(), n, d, mp, A.METRIC["euclidean"], A.CORE_EXCL_SELF,
-                                           core.data_ptr()), "core distances")
-        core_h.copy_(core, non_blocking=True)
+    X_bufs = [X_res, torch.empty_like(X_res)]
+    h2d_s = torch.cuda.Stream()
+    h2d_ev = [None, None]
+
+    def prefetch(j):
+        """step j's points from pinned host memory into buffer j % 2 on the copy stream (its
+        last reader, step j - 2, is queued on the compute stream before this wait)"""
+        h2d_s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(h2d_s):
+            X_bufs[j % 2].copy_(X_pin, non_blocking=True)
+            h2d_ev[j % 2] = torch.cuda.Event()
+            h2d_ev[j % 2].record()
+
+    def run(steps, resident):
+        """steps back to back; not resident: every step uploads its 2 GB of points from pinned
+        host memory (prefetched one step ahead on a copy stream, double-buffered)"""
+        if not resident:
+            prefetch(0)
+        for i in range(steps):
+            if resident:
+                Xd = X_res
+            else:
+                torch.cuda.current_stream().wait_event(h2d_ev[i % 2])
+                Xd = X_bufs[i % 2]
+                if i + 1 < steps:
+                    prefetch(i + 1)
+            core = torch.empty(n, dtype=torch.float64, device="cuda")
+            A.check(A.lib().hdb_core_distances(ctx.h, Xd.data_ptr(), n, d, mp, A.METRIC["euclidean"],
+                                               A.CORE_EXCL_SELF, core.data_ptr()), "core distances")
+            core_h.copy_(core, non_blocking=True)
+            torch.cuda.current_stream().synchronize()  # the step's cores are on the host
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+    run(args.warmup, resident=False)
+    run(1, resident=True)
+    # the value: points in pinned host memory -> H2D -> K1m -> D2H of the cores (SURVEY 8(d))
+    t0 = time.perf_counter()
+    run(args.steps, resident=False)
+    dt = (time.perf_counter() - t0) / args.steps
+    # X already resident in HBM (beside the value, never as it); its HIP events time the kernels
     ctx.set_timing(True)
     for name in ("knn_mfma", "knn_mfma_final", "knn_mfma_order"):
         ctx.kernel_time(name)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.steps
+    run(args.steps, resident=True)
+    dt_hbm = (time.perf_counter() - t0) / args.steps
     k_ms, k_calls = ctx.kernel_time("knn_mfma")
     f_ms, _ = ctx.kernel_time("knn_mfma_final")
     o_ms, _ = ctx.kernel_time("knn_mfma_order")
     ctx.set_timing(False)
-    # the same steps from pinned host memory (the 2 GB H2D inside: PCIe-inclusive, never the value)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(resident=False)
-    torch.cuda.synchronize()
-    dt_pcie = (time.perf_counter() - t0) / args.steps
     k_s = k_ms / 1e3 / args.steps  # K1m screen kernel time of one step (HIP events on its stream)
     blocks = ctx.get_stat("knn_mfma_blocks")  # (query group, 32-candidate block) pairs of the last call
     rows = ctx.get_stat("knn_mfma_group_rows")
@@ -223,12 +245,13 @@ def run_c4(args):
             "data": f"synthetic (L2-normalised embeddings, {C4['centers']} centers + N(0, {C4['noise']}^2), seed {C4['seed']})",
             "config": {"workload": "config 4: 2M x 128 embeddings, core distances minPts 16 (EXCL_SELF) on the MFMA path",
                        "points": n, "d": d, "min_pts": mp,
-                       "timed": "X resident in HBM -> K1m core distances -> D2H of the cores"},
-            "pcie_inclusive_points_per_s": n / dt_pcie, "pcie_inclusive_ms_per_step": dt_pcie * 1e3,
-            "pcie_inclusive_kind": "the same step from pinned host X (2 GB H2D inside the timed region)",
-            "mrd_evals_per_s": n * (n - 1) / dt,
-            "mrd_evals_per_s_kind": "algorithmic-equivalent: n(n-1) pairs of the k-NN over the step time",
-            "executed_pair_evals_per_s": pairs / dt,
+                       "timed": "X in pinned host memory -> H2D (2 GB, prefetched one step ahead on a copy "
+                                "stream) -> K1m core distances -> D2H of the cores"},
+            "hbm_resident_points_per_s": n / dt_hbm, "hbm_resident_ms_per_step": dt_hbm * 1e3,
+            "hbm_resident_kind": "the same steps from X already resident in HBM (no H2D; not the value)",
+            "mrd_evals_per_s": pairs / dt,
+            "mrd_evals_per_s_kind": "executed: (query, candidate) pairs the MFMA screen computes, over the step time",
+            "all_pairs_equivalent_evals_per_s": n * (n - 1) / dt,
             "roofline": {"bound": "mfma", "kernel": "knn_mfma_screen_kernel (K1m)", "achieved": issued / k_s / 1e12,
                          "peak": MFMA_BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                          "frac": issued / k_s / 1e12 / MFMA_BF16_DENSE_TFLOPS,
@@ -302,26 +325,47 @@ CPU_SAMPLES = {  # the partitioned configs' family at a size the serial oracle r
 }
 
 
-def partitioned_cpu_baseline(workload):
-    """The oracle's MR-HDBSCAN* loop (oracle/mr_driver.py over hdb_oracle.c, -O2, one thread:
-    the reference runs one Spark task per subset and setMaster("local") is one thread,
-    Main.java:89) on a 50k-point instance of the config's family, samples per subset and
-    processing_units scaled down with it; flat labels left out (the reference never computes
-    them).  points/s of that instance -- the loop is superlinear in n, so the full-size CPU
-    rate would be lower still."""
-    from oracle import mr_driver as M
+def cpu_sample_instance(workload):
     cs = CPU_SAMPLES[workload]
     rng = np.random.default_rng(cs["seed"])
     C = rng.uniform(-cs["spread"], cs["spread"], size=(cs["centers"], cs["d"]))
-    X = C[rng.integers(0, cs["centers"], size=cs["n"])] + rng.normal(0, 1.0, size=(cs["n"], cs["d"]))
-    t0 = time.perf_counter()
-    r = M.run(X, min_pts=MIN_PTS, min_cl_size=MIN_CL_SIZE, processing_units=cs["processing_units"],
+    return cs, C[rng.integers(0, cs["centers"], size=cs["n"])] + rng.normal(0, 1.0, size=(cs["n"], cs["d"]))
+
+
+def partitioned_cpu_baseline(workload, gpu_run=None):
+    """The oracle's MR-HDBSCAN* loop (oracle/mr_driver.py over hdb_oracle.c, -O2) on a 50k-point
+    instance of the config's family (samples per subset and processing_units scaled down with
+    it; flat labels left out: the reference never computes them), timed twice on the same
+    instance: CPU-all -- a thread pool of the affinity mask's threads over each level's
+    independent subsets and the nearest-sample row chunks (Spark local[*]'s stand-in, one task
+    per subset, Main.java:89,166-169) -- and one thread (setMaster("local"), what the reference
+    runs).  gpu_run(X, cs) -> seconds: the device driver on the same instance, so the three
+    rates compare like for like (the loop is superlinear in n: the full-size CPU rate would be
+    lower still)."""
+    from oracle import mr_driver as M
+    cs, X = cpu_sample_instance(workload)
+    threads = host_threads()
+    kw = dict(min_pts=MIN_PTS, min_cl_size=MIN_CL_SIZE, processing_units=cs["processing_units"],
               samples_per_subset=cs["samples_per_subset"], flat=False)
-    dt = time.perf_counter() - t0
-    return {"value": cs["n"] / dt, "unit": "points/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
-            "sample": f"oracle MR-HDBSCAN* loop (mr_driver, C -O2, 1 thread) on {cs['n']} x {cs['d']} blobs "
-                      f"({cs['centers']} centres, seed {cs['seed']}), samples/subset {cs['samples_per_subset']}, "
-                      f"processing_units {cs['processing_units']}: {r['iterations']} levels in {dt:.1f} s"}
+    t0 = time.perf_counter()
+    r = M.run(X, workers=threads, **kw)
+    dt_all = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    M.run(X, **kw)
+    dt_1 = time.perf_counter() - t0
+    inst = (f"{cs['n']} x {cs['d']} blobs ({cs['centers']} centres, seed {cs['seed']}), samples/subset "
+            f"{cs['samples_per_subset']}, processing_units {cs['processing_units']}, {r['iterations']} levels")
+    out = {"value": cs["n"] / dt_all, "unit": "points/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+           "affinity_cpus": len(os.sched_getaffinity(0)),
+           "sample": f"oracle MR-HDBSCAN* loop (mr_driver, C -O2), thread pool of {threads} over each level's "
+                     f"subsets and nearest-sample row chunks, on {inst}: {dt_all:.1f} s",
+           "single_thread": {"value": cs["n"] / dt_1, "cores": 1, "sample": f"the same instance, 1 thread: {dt_1:.1f} s"}}
+    if gpu_run is not None:
+        dt_g = gpu_run(X, cs)
+        out["gpu_same_instance"] = {"value": cs["n"] / dt_g, "unit": "points/s",
+                                    "sample": f"the device driver on the same instance (1 GPU, flat labels included): "
+                                              f"{dt_g * 1e3:.1f} ms"}
+    return out
 
 
 def predicted_scaling(drv, par, ns=(1, 2, 4, 8)):
@@ -473,7 +517,23 @@ def run_partitioned(args, workload):
                 if args.phases and world == 1 else None,
                 "roofline": partitioned_roofline(kt, coop_steps, coop_launches, args.steps)}
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = partitioned_cpu_baseline(workload)
+            def gpu_run(Xs, cs):
+                d2 = pkg.MRHDBSCANStar(minPts=MIN_PTS, minClSize=MIN_CL_SIZE, processing_units=cs["processing_units"],
+                                       samples_per_subset=cs["samples_per_subset"])
+                Xp = torch.from_numpy(Xs).pin_memory()
+                best = None
+                for i in range(3):  # the first run warms the instance's kernels; best of the other two
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    r2 = d2.run(Xp.to("cuda", non_blocking=True))
+                    [x.to("cpu") for x in r2["edges"]]
+                    r2["labels"].to("cpu")
+                    torch.cuda.synchronize()
+                    dt2 = time.perf_counter() - t0
+                    if i:
+                        best = dt2 if best is None else min(best, dt2)
+                return best
+            line["cpu_baseline"] = partitioned_cpu_baseline(workload, gpu_run)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -659,12 +719,16 @@ def main():
                 st = pkg.HDBSCANStar(c)
                 self.ctxs[j] = c
                 self.ready.wait()
+                Xw = torch.empty_like(X_res)  # this worker's point buffer (H2D target)
                 while True:
-                    i = self.qs[j].get()
-                    if i is None:
+                    job = self.qs[j].get()
+                    if job is None:
                         return
+                    i, resident = job
                     try:
-                        _, mst = st.exactMST(X_res, MIN_PTS, None, pkg.CORE_EXCL_SELF, True)
+                        if not resident:  # the step's points uploaded from pinned host memory
+                            Xw.copy_(X_pin, non_blocking=True)
+                        _, mst = st.exactMST(X_res if resident else Xw, MIN_PTS, None, pkg.CORE_EXCL_SELF, True)
                         own = pkg.sort_edges_desc(mst.getVerticeA(), mst.getVericeB(), mst.getEges(), c)
                         ev = torch.cuda.Event()
                         ev.record()
@@ -675,8 +739,8 @@ def main():
                         self.res[i] = out
                         self.cv.notify_all()
 
-        def submit(self, i):
-            self.qs[i % self.m].put(i)
+        def submit(self, i, resident):
+            self.qs[i % self.m].put((i, resident))
 
         def result(self, i):
             with self.cv:
@@ -740,13 +804,13 @@ def main():
         resident: the points are already in HBM (no H2D: the value's timed region);
         otherwise every step uploads its points from pinned host memory first"""
         i0 = pipe["next"]
-        if resident and workers is not None:  # M partitions in flight in stage 1
+        if workers is not None:  # M partitions in flight in stage 1 (each uploads its own points)
             for i in range(i0, min(i0 + M, i0 + steps)):
-                workers.submit(i)
+                workers.submit(i, resident)
             for i in range(i0, i0 + steps):
                 ev, own = workers.result(i)
                 if i + M < i0 + steps:
-                    workers.submit(i + M)
+                    workers.submit(i + M, resident)
                 torch.cuda.current_stream().wait_event(ev)
                 merged = par.gather_sorted_msts(*own, dst=0) if world > 1 else own
                 stage.submit(own, merged if rank == 0 else None)
@@ -779,51 +843,38 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    pipe_run(args.warmup, resident=True)
-    pipe_run(1)  # the H2D path warm too
+    pipe_run(args.warmup)
+    pipe_run(1, resident=True)  # the HBM-resident path warm too
     barrier()
-    # per-kernel device times: HIP events recorded on the launch streams inside the timed
-    # region (measured cost of the records: ~1% of a step)
-    keys = ("knn_tree", "boruvka_total", "boruvka_scan", "merge_sort")
-    s1 = workers.ctxs if workers is not None else [ctx]  # stage-1 contexts
-    for c in (*s1, *stage.ctxs):
-        c.set_timing(True)
-    for k in keys:
-        for c in s1:
-            c.kernel_time(k)
-    for c in stage.ctxs:
-        c.kernel_time("flat_labels")
+    # the value: every step's points uploaded from pinned host memory inside the timed region
+    # (from parsed points resident in host memory)
+    t0 = time.perf_counter()
+    pipe_run(args.steps)
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    # the same pipeline from points already resident in HBM (reported beside the value, never as it)
     barrier()
     t0 = time.perf_counter()
     pipe_run(args.steps, resident=True)
     barrier()
-    dt = max_over_ranks(time.perf_counter() - t0)
-    for c in (*s1, *stage.ctxs):
-        c.set_timing(False)
-    kt = {}
-    for k in keys:
-        tm = [c.kernel_time(k) for c in s1]
-        kt[k] = (sum(t[0] for t in tm), sum(t[1] for t in tm))
-    tl = [c.kernel_time("flat_labels") for c in stage.ctxs]
-    kt["flat_labels"] = (sum(t[0] for t in tl), sum(t[1] for t in tl))
-    # the same pipeline with every step's points uploaded from pinned host memory
-    # (PCIe-inclusive; reported beside the value, never as it)
-    barrier()
-    t0 = time.perf_counter()
-    pipe_run(args.steps)
-    barrier()
-    dt_pcie = max_over_ranks(time.perf_counter() - t0)
+    dt_hbm = max_over_ranks(time.perf_counter() - t0)
     stage.close()
     if workers is not None:
         workers.close()
-    # latency of one step without the pipeline (each step's stages back to back)
+    # latency of one step without the pipeline (each step's stages back to back); its HIP
+    # events time the flat labels of one partition alone
+    keys = ("knn_tree", "boruvka_total", "boruvka_scan", "merge_sort")
     step_e2e()
     barrier()
+    ctx.set_timing(True)
+    ctx.kernel_time("flat_labels")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step_e2e()
     barrier()
     dt_lat = max_over_ranks(time.perf_counter() - t0)
+    kt_lab = ctx.kernel_time("flat_labels")
+    ctx.set_timing(False)
     # the same pipeline from HBM-resident points to HBM-resident merged edges, one partition at
     # a time: its HIP events time each kernel alone (the roofline's kernel duration; in the
     # pipelined region several partitions overlap and an event pair also spans other streams')
@@ -873,7 +924,9 @@ def main():
 
     total_points = world * n
     value = total_points * tsteps / dt
-    ms = {k: v[0] / tsteps for k, v in kt.items()}
+    # per-partition kernel times, each kernel alone (one partition at a time: the device-resident
+    # pass for stage 1, the latency pass for the labels)
+    ms = {k: v[0] / tsteps for k, v in kt_seq.items()} | {"flat_labels": kt_lab[0] / tsteps}
     scan_ms, scan_n = kt_seq["boruvka_scan"]
     avg_scan_s = scan_ms / max(scan_n, 1) / 1e3
     # Latency roofline of the dominant kernel (the K2b scan): every node or leaf visit needs
@@ -905,7 +958,8 @@ def main():
         "data": "synthetic (seeded Gaussian blobs, 20 centers ~U[-100,100]^3, sigma 1, seed 1+rank)",
         "config": {"workload": "config 2: blobs 1M x 3 exact HDBSCAN* (no sampling), minPts 4, minClSize 4",
                    "points_per_gpu": n, "d": D, "min_pts": MIN_PTS, "min_cl_size": MIN_CL_SIZE,
-                   "core": "EXCL_SELF", "timed": "X resident in HBM -> K1t cores -> K2b MST + self edges "
+                   "core": "EXCL_SELF", "timed": "X in pinned host memory -> H2D (each stage-1 worker uploads "
+                   "its step's points on its own stream) -> K1t cores -> K2b MST + self edges "
                    "-> merge sort (N>1: per-rank sort, gather to rank 0, merge of the presorted runs) -> "
                    "K6 flat labels of the partition (D2H of the merged list overlapping it on a copy "
                    "stream) -> D2H of the labels; pipelined: step i's labels + D2H (own thread, stream and "
@@ -914,10 +968,9 @@ def main():
                    "stage1_partitions_in_flight": M, "label_stages": L,
                    "parallelism": f"partition-sharded x{world}"},
         "n_clusters": n_clusters[0],
-        "pcie_inclusive_points_per_s": total_points * tsteps / dt_pcie,
-        "pcie_inclusive_ms_per_step": dt_pcie * 1e3 / tsteps,
-        "pcie_inclusive_kind": "the same pipeline with each step's points uploaded from pinned host memory "
-                               "(H2D on a copy stream, prefetched one step ahead)",
+        "hbm_resident_points_per_s": total_points * tsteps / dt_hbm,
+        "hbm_resident_ms_per_step": dt_hbm * 1e3 / tsteps,
+        "hbm_resident_kind": "the same pipeline from points already resident in HBM (no H2D; not the value)",
         "latency_ms_per_step": dt_lat * 1e3 / tsteps,
         "latency_kind": "the same steps without the pipeline: each step's stages back to back",
         "device_resident_points_per_s": total_points * tsteps / dt_dev,
@@ -927,7 +980,9 @@ def main():
                                 "8(d)) over the step time; the exact pruned kernels execute ~1/1000 of it "
                                 "(executed_pair_evals_per_s)",
         "executed_pair_evals_per_s": world * (knn_evals + bor_evals) * tsteps / dt,
-        "kernels_ms_per_step": ms,
+        "kernels_ms_per_partition": ms,
+        "kernels_kind": "HIP events on the launch stream, one partition at a time (stage 1: the device-resident "
+                        "pass; flat_labels: the latency pass); boruvka_total includes boruvka_scan",
         "executed_pair_evals_per_step": {"knn_tree": knn_evals, "boruvka_scan": bor_evals,
                                          "algorithmic": n * n + n * (n - 1) // 2},
         "roofline": {"bound": "latency", "kernel": "boruvka_scan (boruvka_bvh_kernel)",

@@ -41,10 +41,40 @@ def sample_ids(n_key: int, k: float, samples_per_subset: int | None, seed: int, 
     return np.sort(rng.choice(n_key, size=m, replace=False)).astype(np.int64)
 
 
+def _nearest_chunked(P, S, metric, pool, workers):
+    """nearest_sample over row chunks on the pool (each point's first minimum is independent
+    of the others: identical to one call)"""
+    if pool is None or P.shape[0] < 4 * workers:
+        return O.nearest_sample(P, S, metric)[0]
+    cuts = np.linspace(0, P.shape[0], workers + 1).astype(np.int64)
+    parts = pool.map(lambda i: O.nearest_sample(P[cuts[i]:cuts[i + 1]], S, metric)[0], range(workers))
+    return np.concatenate(list(parts))
+
+
 def run(X, min_pts=4, min_cl_size=4, processing_units=50, k=0.2, samples_per_subset=None, seed=20210101,
-        metric="euclidean", all_inter_edges=True, max_levels=64, log=None, flat=True):
+        metric="euclidean", all_inter_edges=True, max_levels=64, log=None, flat=True, workers=1):
     """Returns dict(edges=(va, vb, w) merged (stable, descending weight), levels=[...],
-    leaf_of=np.array subset key of the leaf that processed each point, iterations)."""
+    leaf_of=np.array subset key of the leaf that processed each point, iterations).
+
+    workers > 1: the CPU-all variant (Spark local[*]'s stand-in, Main.java:89 with one task per
+    subset): a level's leaves run concurrently, its big subsets' nearest sample + bubble stats +
+    local model run concurrently (the nearest-sample scan of one subset also split into row
+    chunks), on a thread pool over the C oracle (ctypes releases the GIL); the bookkeeping that
+    numbers the new subsets stays sequential in key order, so the result is identical."""
+    pool = None
+    if workers > 1:
+        import concurrent.futures as cf
+        pool = cf.ThreadPoolExecutor(workers)
+    try:
+        return _run(X, min_pts, min_cl_size, processing_units, k, samples_per_subset, seed, metric,
+                    all_inter_edges, max_levels, log, flat, pool, workers)
+    finally:
+        if pool is not None:
+            pool.shutdown()
+
+
+def _run(X, min_pts, min_cl_size, processing_units, k, samples_per_subset, seed, metric, all_inter_edges,
+         max_levels, log, flat, pool, workers):
     X = np.ascontiguousarray(X, np.float64)
     n, d = X.shape
     key_of = np.zeros(n, np.int64)            # MapperDataset_github.java:20: key 0
@@ -74,12 +104,12 @@ def run(X, min_pts=4, min_cl_size=4, processing_units=50, k=0.2, samples_per_sub
                 f"max {max(level['leaves'].values(), default=0)}), {len(big_keys)} big subsets "
                 f"({sum(level['big'].values())} pts)")
         # FirstStep leaf branch (FirstStep.java:104-120)
-        leaf_edges = []
-        for c in leaf_keys:
+        def leaf(c):
             rows = members[c]
-            _, (va, vb, w) = O.first_step_leaf(X[rows], rows.astype(np.int32), min_pts, metric)
-            leaf_edges.append((va, vb, w))
-            leaf_of[rows] = c
+            return O.first_step_leaf(X[rows], rows.astype(np.int32), min_pts, metric)[1]
+        leaf_edges = list(pool.map(leaf, leaf_keys)) if pool is not None else [leaf(c) for c in leaf_keys]
+        for c in leaf_keys:
+            leaf_of[members[c]] = c
         edge_lists.extend(leaf_edges)
         iteration += 1
         if processed >= n:
@@ -89,24 +119,32 @@ def run(X, min_pts=4, min_cl_size=4, processing_units=50, k=0.2, samples_per_sub
         inter_edges = []
         new_alive = np.zeros(n, bool)
         new_key = np.full(n, -2, np.int64)
-        for c in big_keys:
+        def model(c):
             rows = members[c]
             sp = sample_ids(rows.shape[0], k, samples_per_subset, seed, iteration - 1, c)
             S = X[rows[sp]]
-            nearest, _ = O.nearest_sample(X[rows], S, metric)
+            nearest = _nearest_chunked(X[rows], S, metric, pool if len(big_keys) == 1 else None, workers)
             # CombineStep per (subset, sample): fold in ascending global id (D5)
             st = O.bubble_stats(X[rows], nearest, S.shape[0], "combine")
             nonempty = np.nonzero(st["info"][:, 2] > 0)[0]  # D4 (a 1-member bubble keeps [0, 0, 1])
-            pos = np.full(S.shape[0], -1, np.int64)
-            pos[nonempty] = np.arange(nonempty.shape[0])
-            rep = st["rep"][nonempty]
-            info = st["info"][nonempty]
-            lm = None
+            lm, err = None, None
             if nonempty.shape[0] >= 2:
                 try:
-                    lm = O.local_model(rep, info, min_pts, min_cl_size, metric)  # LocalModelReduceByKey.java:88-104
+                    lm = O.local_model(st["rep"][nonempty], st["info"][nonempty], min_pts, min_cl_size,
+                                       metric)  # LocalModelReduceByKey.java:88-104
                 except O.OracleError as e:                 # D10: the reference throws here
-                    level.setdefault("model_errors", {})[c] = e.code
+                    err = e.code
+            return sp, nearest, nonempty, lm, err
+        if pool is not None and len(big_keys) > 1:
+            results = list(pool.map(model, big_keys))
+        else:
+            results = [model(c) for c in big_keys]
+        for c, (sp, nearest, nonempty, lm, err) in zip(big_keys, results):
+            rows = members[c]
+            if err is not None:
+                level.setdefault("model_errors", {})[c] = err
+            pos = np.full(sp.shape[0], -1, np.int64)
+            pos[nonempty] = np.arange(nonempty.shape[0])
             if lm is None:                                 # one bubble (reducer never runs) or D10
                 labels = np.full(nonempty.shape[0], 2, np.int32)
             else:

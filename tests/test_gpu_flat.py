@@ -142,3 +142,37 @@ def test_device_comb_cluster_tree_equal_host(pkg, ctx, teeth, tie):
         ref, kr = lib_flat(pkg, va[d], vb[d], w[d], n, mcs)
         got, kg = dev_flat(pkg, ctx, va[d], vb[d], w[d], n, mcs)
         assert kg == kr and np.array_equal(got, ref), (teeth, tie, mcs)
+
+
+@pytest.mark.parametrize("shape", ["tied_path", "shedding_path", "comb200k"])
+def test_device_long_chains_equal_host(pkg, ctx, shape):
+    """chains far longer than the ~3k of the tests above: every pointer-jumping pass (tie tops,
+    cluster starts, the FOSC heavy paths and the selection) must converge within its launch
+    budget, which is sized from the reach a launch guarantees under stale reads
+    and checked on the device (HDB_EDEVICE otherwise).
+    tied_path: 1M points on a path, every edge weight equal (one tie node of depth ~1M);
+    shedding_path: 1M-point path with increasing weights (one cluster shedding a point per
+    level: a cluster-start chain ~1M long); comb200k: 200k teeth of 5 points on a spine of
+    increasing weights (a 200k-cluster caterpillar: heavy path and selection chains ~200k)"""
+    rng = np.random.default_rng(11)
+    if shape == "comb200k":
+        teeth, tooth = 200_000, 5
+        base = np.arange(teeth, dtype=np.int64) * tooth
+        ta = np.repeat(base, tooth - 1)
+        tb = (base[:, None] + np.arange(1, tooth)[None, :]).ravel()
+        tw = rng.random(ta.shape[0]) * 0.5
+        sa, sb = base[:-1], base[1:]
+        sw = 1.0 + np.arange(teeth - 1, dtype=np.float64)
+        va, vb, w = np.r_[ta, sa], np.r_[tb, sb], np.r_[tw, sw]
+        n = teeth * tooth
+    else:
+        n = 1_000_000
+        va, vb = np.arange(n - 1), np.arange(1, n)
+        w = np.ones(n - 1) if shape == "tied_path" else np.arange(n - 1, dtype=np.float64)
+    perm = rng.permutation(n)
+    va, vb = perm[va].astype(np.int32), perm[vb].astype(np.int32)
+    d = np.argsort(-w, kind="stable")
+    for mcs in (2, 5):
+        ref, kr = lib_flat(pkg, va[d], vb[d], w[d], n, mcs)
+        got, kg = dev_flat(pkg, ctx, va[d], vb[d], w[d], n, mcs)
+        assert kg == kr and np.array_equal(got, ref), (shape, mcs)

@@ -126,3 +126,35 @@ def test_mfma_lists_equal_fp64_200k_x_128(pkg, ctx, star):
     ref = lists(ctx, star, X, k, False)
     assert got.shape == (n, k)
     assert torch.equal(got.view(torch.int64), ref.view(torch.int64))
+
+
+def test_mfma_cores_full_size_c4_rows(pkg, ctx, star):
+    """BASELINE config 4 at full size: 2M x 128 L2-normalised embeddings (bench.py's seeded
+    generator), minPts 16, EXCL_SELF core distances through the default path (the MFMA screen
+    + FP64 re-check).  64 sampled rows must equal, bit for bit, the (minPts-1)-th smallest
+    Java-order distance over all 2M rows (CreateLocalMST.java:138-185: sequential sum of
+    (a-b)*(a-b) in dimension order, no FMA -- every step here is its own elementwise kernel,
+    so each sub, mul and add rounds once) with the query itself excluded."""
+    import torch
+    n, d, mp, centers = 2_000_000, 128, 16, 200
+    g = torch.Generator(device="cuda").manual_seed(4)
+    C = torch.randn(centers, d, dtype=torch.float64, device="cuda", generator=g)
+    lab = torch.randint(0, centers, (n,), device="cuda", generator=g)
+    X = C[lab] + 0.1 * torch.randn(n, d, dtype=torch.float64, device="cuda", generator=g)
+    X = (X / torch.linalg.norm(X, dim=1, keepdim=True)).contiguous()
+    del C, lab
+    got = star.calculateCoreDistances(X, mp, None, pkg.CORE_EXCL_SELF)
+    torch.cuda.synchronize()
+    assert ctx.get_stat("knn_mfma_blocks") > 0  # the MFMA path ran (not the FP64 fallback)
+    rows = torch.from_numpy(np.random.default_rng(44).choice(n, 64, replace=False)).cuda()
+    Q = X[rows]                                  # 64 x 128
+    s = torch.zeros(64, n, dtype=torch.float64, device="cuda")
+    for j in range(d):
+        t = Q[:, j:j + 1] - X[:, j].unsqueeze(0)  # 64 x n
+        s += t * t
+        del t
+    s[torch.arange(64, device="cuda"), rows] = float("inf")
+    ref = torch.sqrt(torch.kthvalue(s, mp - 1, dim=1).values)
+    assert torch.equal(got[rows].view(torch.int64), ref.view(torch.int64)), \
+        (got[rows] - ref).abs().max().item()
+    assert bool(torch.isfinite(got).all()) and bool((got >= 0).all())
