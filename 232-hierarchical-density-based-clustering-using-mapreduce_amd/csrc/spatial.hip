@@ -493,6 +493,39 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
     }
 }
 
+#ifndef HDB_BOR_PROF
+#define HDB_BOR_PROF 0  // diagnostic build: per-wave cycle split of the K2b scan (stats boruvka_prof_*)
+#endif
+// Cycle split of one wave's scan (HDB_BOR_PROF, STATS instantiation only): mark(k) charges the
+// shader cycles since the previous mark to phase k.  Phases: 0 setup, 1 pop + bound refresh,
+// 2 internal-node box staging (the dependent global load), 3 child tests, 4 ranking + push,
+// 5 leaf record/group-box staging, 6 leaf group mask, 7 leaf candidate loops, 8 bound publish,
+// 9 tail (best writes, component minimum).
+constexpr int BOR_PROF_N = 10;
+constexpr int BOR_STATS_HDR = 32;  // stats: [0..4] sums, [16..25] cycle split, then one word per wave
+template <bool ON>
+struct BorProf {
+    unsigned long long pc[BOR_PROF_N];
+    long long last;
+    __device__ __forceinline__ void start() {
+        if (ON) {
+#pragma unroll
+            for (int k = 0; k < BOR_PROF_N; k++) pc[k] = 0;
+            last = clock64();
+        }
+    }
+    __device__ __forceinline__ void mark(int k) {
+        if (ON) {
+            const long long now = clock64();
+            pc[k] += (unsigned long long)(now - last);
+            last = now;
+        }
+    }
+};
+struct NoProf {
+    __device__ __forceinline__ void mark(int) {}
+};
+
 // Pushes the children of internal node (lev, idx) that some lane needs, farthest first
 // (so the nearest is popped first), ordered by box-to-box distance from the query box.
 // needs(a, b, tag): does this lane need the box [a, b] with that tag.  The per-child test
@@ -549,15 +582,17 @@ __device__ __forceinline__ void push_children(const Bvh &bvh, const int64_t *off
 // its 8-lane subgroup L >> 3 (ok(a, b, tag): a superset of what the subgroup's lanes need),
 // then only the children that pass are tested per lane (needs) -- the same children as
 // push_children, with one wave-wide test plus one per surviving child instead of one per child.
-template <int D, class SubOk, class Needs>
+template <int D, class SubOk, class Needs, class Prof = NoProf>
 __device__ __forceinline__ void push_children_sub(const Bvh &bvh, const int64_t *off_s, const int64_t *cnt_s, int lev,
                                                   int64_t idx, const double *qlo, const double *qhi, int32_t *stk,
-                                                  int &sp, int lane, double *sb, int32_t *st, SubOk ok, Needs needs) {
+                                                  int &sp, int lane, double *sb, int32_t *st, SubOk ok, Needs needs,
+                                                  Prof &&prof = NoProf{}) {
     const int64_t c0 = idx * FAN;
     const int64_t c1 = min(c0 + FAN, cnt_s[lev - 1]);
     const int64_t base = off_s[lev - 1] + c0;
     const int nc = (int)(c1 - c0);
     stage_boxes<D, FAN>(bvh.lo + base * D, bvh.hi + base * D, bvh.tag + base, nc, sb, st, lane);
+    prof.mark(2);
     const int k = lane & (FAN - 1);
     bool need = false;
     if (k < nc) {
@@ -584,6 +619,7 @@ __device__ __forceinline__ void push_children_sub(const Bvh &bvh, const int64_t 
         if (__any(needs(a, b, st[kk]))) okmask |= 1u << kk;
     }
     okmask = __builtin_amdgcn_readfirstlane(okmask);
+    prof.mark(3);
     if (okmask == 0) return;
     double key = -1.0;
     const bool mine = lane < FAN && ((okmask >> lane) & 1u);
@@ -607,6 +643,7 @@ __device__ __forceinline__ void push_children_sub(const Bvh &bvh, const int64_t 
     if (mine) stk[sp + rank] = ((lev - 1) << 26) | (int32_t)(c0 + lane);
     __builtin_amdgcn_wave_barrier();
     sp += __popc(okmask);
+    prof.mark(4);
 }
 
 // Publishes min(v) per component into arr with few atomics: late rounds put most of the
@@ -664,6 +701,8 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
     if (t >= *nwaves) return;
     if (*n_edges_done >= (unsigned long long)(n - 1)) return;  // speculative round after the last
     const long long t_start = STATS ? clock64() : 0;
+    BorProf<STATS && HDB_BOR_PROF> prof;
+    prof.start();
     LRec<D> *cand = tile_s[w];
     const int lane = threadIdx.x & 63;
     int32_t *stk = stack_s[w];
@@ -817,6 +856,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
     int32_t pf_code = -1;  // stack code of the leaf held in pf
     LeafRegs<D> pf;
 #endif
+    prof.mark(0);
     while (sp > 0) {
         __builtin_amdgcn_wave_barrier();
         const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
@@ -825,6 +865,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
         const int64_t idx = code & ((1 << 26) - 1);
         const int64_t node = off_s[lev] + idx;
         if ((visits++ & 7) == 0) refresh();
+        prof.mark(1);
         // re-test the popped node with the current bound (its parent tested it when pushing)
         if (pop_test & 1) {
             stage_boxes<D, 1>(bvh.lo + node * D, bvh.hi + node * D, bvh.tag + node, 1, bxs, bxt, lane);
@@ -835,7 +876,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
         if (lev > 0) {
 #if HDB_BOR_SUBTEST
             push_children_sub<D>(bvh, off_s, cnt_s, lev, idx, qlo, qhi, stk, sp, lane, bxs, bxt, sub_ok(sub_bound()),
-                                 needs_vals);
+                                 needs_vals, prof);
 #else
             push_children<D>(bvh, off_s, cnt_s, lev, idx, qlo, qhi, stk, sp, lane, bxs, bxt, needs_vals);
 #endif
@@ -872,6 +913,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
         cand[lane] = mine;  // staged now: the record's registers die before the culling
         __builtin_amdgcn_wave_barrier();
 #endif
+        prof.mark(5);
         auto gneeds = [&](int gi) -> bool {
             double a[D], bb[D];
             staged_box<D, NSG>(bxs, gi, a, bb);
@@ -879,6 +921,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
         };
 #if HDB_BOR_SUBTEST
         const unsigned gmask = group_mask();  // pre-filter; the per-lane test below decides
+        prof.mark(6);
 #else
         unsigned gmask = 0;
 #pragma unroll 1
@@ -914,6 +957,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
                 }
             }
         }
+        prof.mark(7);
         if (found) {
             const double c2 = (b.w * b.w) * (1.0 + 1e-12);
             if (c2 < cb2) {
@@ -924,6 +968,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
                 if (b.w < cwv) cwv = b.w;
             }
         }
+        prof.mark(8);
     }
     if (valid) {
         best_w[i] = b.w;
@@ -941,6 +986,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
         xact[i] = (!(mlb > cwv) && b.w <= cwv) ? 1 : 0;
     }
     publish_min(comp_w, mcomp, dbits(b.w), valid && b.w < INFINITY);
+    prof.mark(9);
     if (STATS) {
         for (int off = 32; off >= 1; off >>= 1) nev += __shfl_xor(nev, off);
         const unsigned long long act_mask = __ballot(active0);
@@ -950,7 +996,10 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
             atomicAdd(&stats[2], (unsigned long long)visits);
             atomicAdd(&stats[3], (unsigned long long)__popcll(act_mask));  // lanes searching at start
             atomicAdd(&stats[4], (unsigned long long)(act_mask != 0));     // waves with any such lane
-            stats[8 + t] = (unsigned long long)(clock64() - t_start);        // per-wave shader cycles
+#if HDB_BOR_PROF
+            for (int k = 0; k < BOR_PROF_N; k++) atomicAdd(&stats[16 + k], prof.pc[k]);
+#endif
+            stats[BOR_STATS_HDR + t] = (unsigned long long)(clock64() - t_start);  // per-wave shader cycles
         }
     }
 }
@@ -1753,7 +1802,7 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
     int32_t *gcnt = ex.take<int32_t>(ngroups), *gwaves = ex.take<int32_t>(ngroups), *woff = ex.take<int32_t>(ngroups);
     unsigned long long *desc = ex.take<unsigned long long>(max_waves);
     int32_t *nwaves = ex.take<int32_t>(1);
-    unsigned long long *evals = ctx->count_evals ? ex.take<unsigned long long>(8 + max_waves) : nullptr;
+    unsigned long long *evals = ctx->count_evals ? ex.take<unsigned long long>(BOR_STATS_HDR + max_waves) : nullptr;
     int64_t tot_evals = 0;
     Rec<D> *recs = sp.recs;
     int32_t *inv = sp.inv;
@@ -1826,7 +1875,7 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
                            tcomp + bvh.off[1], n_inner);
         hipLaunchKernelGGL(retag_kernel<D>, dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, st, recs, pcomp, n,
                            ntiles, bvh.levels, round > 0 ? parent2 : nullptr, tcomp, bvh.stag);
-        if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 8 * (8 + max_waves), st));
+        if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 8 * (BOR_STATS_HDR + max_waves), st));
         round_seed(round);
         {
             KernelTimer ts(ctx, "boruvka_scan");
@@ -1850,12 +1899,17 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
                                    nwaves, ctx->trav_pop_test, inv, best_pos, n_edges, bs.lbw, bs.xact, evals);
         }
         if (evals) {
-            unsigned long long h[5];
-            HIP_CHECK(hipMemcpyAsync(h, evals, 40, hipMemcpyDeviceToHost, st));
+            unsigned long long h[BOR_STATS_HDR];
+            HIP_CHECK(hipMemcpyAsync(h, evals, 8 * BOR_STATS_HDR, hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
             const std::string r = "boruvka_r" + std::to_string(round);
+            if (HDB_BOR_PROF) {
+                static const char *pn[BOR_PROF_N] = {"setup", "pop", "stage", "test", "push",
+                                                     "leaf_load", "leaf_mask", "leaf_eval", "publish", "tail"};
+                for (int k = 0; k < BOR_PROF_N; k++) ctx->stats[r + "_prof_" + pn[k]] = (int64_t)h[16 + k];
+            }
             wave_cyc.resize(max_waves);
-            HIP_CHECK(hipMemcpyAsync(wave_cyc.data(), evals + 8, 8 * max_waves, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipMemcpyAsync(wave_cyc.data(), evals + BOR_STATS_HDR, 8 * max_waves, hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
             wave_cyc.erase(std::remove(wave_cyc.begin(), wave_cyc.end(), 0ull), wave_cyc.end());  // exited waves
             if (wave_cyc.empty()) wave_cyc.push_back(0);

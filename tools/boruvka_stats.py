@@ -42,3 +42,11 @@ for r in range(12):
         break
     cyc = [ctx.get_stat(p + "_wave_cyc_" + s) for s in ("mean", "p50", "p99", "max")]
     print(f"r{r}: active lanes {vals[0]:>8d}  waves {vals[1]:>6d}  nodes {vals[2]:>9d}  leaves {vals[3]:>8d}  evals {vals[4]:>11d}  wave cyc mean/p50/p99/max {cyc}")
+    try:  # HDB_BOR_PROF build: cycle split summed over the round's waves, per node visit
+        pn = ("setup", "pop", "stage", "test", "push", "leaf_load", "leaf_mask", "leaf_eval", "publish", "tail")
+        pr = [ctx.get_stat(p + "_prof_" + s) for s in pn]
+        tot = sum(pr) or 1
+        print("    cycles/visit " + "  ".join(f"{s} {v / max(vals[2], 1):.0f}" for s, v in zip(pn, pr)) +
+              f"  | share " + " ".join(f"{s} {100 * v / tot:.0f}%" for s, v in zip(pn, pr)))
+    except Exception:
+        pass
