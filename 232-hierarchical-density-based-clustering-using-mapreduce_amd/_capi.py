@@ -23,6 +23,7 @@ ERRORS = {
 
 METRIC = {"euclidean": 0, "cosine": 1, "pearson": 2, "manhattan": 3, "supremum": 4}
 CORE_INCL_SELF_CUMULATIVE, CORE_INCL_SELF, CORE_EXCL_SELF = 0, 1, 2
+EDGES_SELF, EDGES_MERGED = 1, 2  # hdb_exact_mst edge flags (include/hdbmi.h)
 BUBBLE_COMBINESTEP, BUBBLE_CF = 0, 1
 JMAX = float(np.finfo(np.float64).max)
 

@@ -246,7 +246,8 @@ int hdb_exact_mst(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t m
         check_metric(metric);
         if (n < 1 || d <= 0 || !X || !va || !vb || !w) HDB_THROW(HDB_EINVAL, "bad arguments");
         if (semantics < 0 || semantics > 2) HDB_THROW(HDB_EINVAL, "unknown core semantics");
-        const int64_t ne = (n - 1) + (self_edges ? n : 0);
+        if (self_edges & ~(HDB_EDGES_SELF | HDB_EDGES_MERGED)) HDB_THROW(HDB_EINVAL, "unknown edge flags");
+        const int64_t ne = (n - 1) + ((self_edges & HDB_EDGES_SELF) ? n : 0);
         Stager s(ctx);
         const double *dX = s.in(X, n * d);
         double *dc = core_out ? s.out(core_out, n) : (double *)arena(ctx, A_STAGE_OUT, sizeof(double) * (size_t)n);

@@ -40,6 +40,10 @@ void bubble_stats_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const 
 void bubble_knn_device(hdb_ctx *ctx, const double *rep, const double *eB, const double *nnB, int64_t b, int d,
                        int metric, int K, double *knn_out, int32_t *log_out);
 void sort_edges_desc_device(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne);
+// stable merge of two descending runs held in separate arrays (A first on equal weights)
+void merge_two_runs_device(hdb_ctx *ctx, const int32_t *aA, const int32_t *bA, const double *wA, int64_t na,
+                           const int32_t *aB, const int32_t *bB, const double *wB, int64_t nb, int32_t *oa,
+                           int32_t *ob, double *ow);
 // CreateLocalMST record fields: local indices of each edge's vertices in `ids` (synchronises)
 void merge_sorted_runs_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, const double *w,
                               const std::vector<int64_t> &off, int32_t *oa, int32_t *ob, double *ow);

@@ -248,6 +248,17 @@ __global__ __launch_bounds__(MP_TB) void merge_path_kernel(const int32_t *__rest
     }
 }
 
+// two descending runs in separate arrays, A first on equal weights (the exact leaf's merged
+// order: its tree edges and its self edges)
+void merge_two_runs_device(hdb_ctx *ctx, const int32_t *aA, const int32_t *bA, const double *wA, int64_t na,
+                           const int32_t *aB, const int32_t *bB, const double *wB, int64_t nb, int32_t *oa,
+                           int32_t *ob, double *ow) {
+    if (na + nb <= 0) return;
+    hipLaunchKernelGGL(merge_path_kernel, dim3((unsigned)ceil_div(na + nb, (int64_t)MP_T)), dim3(MP_TB), 0, ctx->stream,
+                       aA, bA, wA, na, aB, bB, wB, nb, oa, ob, ow);
+    HIP_CHECK(hipGetLastError());
+}
+
 // precondition check: no NaN, every run non-increasing (bit 0 / bit 1)
 __global__ void runs_check_kernel(const double *__restrict__ w, int64_t ne, const int64_t *__restrict__ run_end_flag,
                                   int *__restrict__ err) {

@@ -1208,6 +1208,15 @@ __global__ void edge_idkey_kernel(const int32_t *a, const int32_t *b, int64_t m,
 __global__ void edge_wkey_kernel(const int32_t *perm_, const double *ww, int64_t m, uint64_t *k) {
     HDB_GRID_STRIDE(i, m) k[i] = (uint64_t)__double_as_longlong(ww[perm_[i]]);
 }
+// self edges' sort keys: the core (+0.0 for -0.0: Java's comparator ties them) and the id
+__global__ void self_keys_kernel(const double *__restrict__ core, int64_t n, double *__restrict__ k,
+                                 int32_t *__restrict__ id) {
+    HDB_GRID_STRIDE(i, n) {
+        const double c = core[i];
+        k[i] = c == 0.0 ? 0.0 : c;
+        id[i] = (int32_t)i;
+    }
+}
 __global__ void edge_out_kernel(const int32_t *perm_, const int32_t *a, const int32_t *b, const double *ww, int64_t m,
                                 int32_t *oa, int32_t *ob, double *ow) {
     HDB_GRID_STRIDE(i, m) {
@@ -1730,7 +1739,8 @@ struct KnnLists {
 // boruvka_extra_bytes(n) region.  kl (nullable): k-NN lists that seed every round.
 template <int D>
 static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extra, const KnnLists *kl,
-                             int32_t *va, int32_t *vb, double *w);
+                             int32_t *va, int32_t *vb, double *w, bool merged = false,
+                             const double *self_core = nullptr);
 
 template <int D>
 struct BoruvkaState {
@@ -1775,7 +1785,7 @@ static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double 
 
 template <int D>
 static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extra, const KnnLists *kl,
-                             int32_t *va, int32_t *vb, double *w) {
+                             int32_t *va, int32_t *vb, double *w, bool merged, const double *self_core) {
     const size_t per = (size_t)n;
     size_t used = 0;
     BoruvkaState<D> bs = boruvka_state<D>(extra, n, &used);
@@ -1971,14 +1981,47 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             void *tmp = arena(ctx, A_SORT, tb);
             HIP_CHECK(sort_pairs(tmp, tb, k1, k2, p1, p2, ne, 0, 2 * B, st));
             hipLaunchKernelGGL(edge_wkey_kernel, dim3(g), dim3(256), 0, st, p2, ew, ne, k1);
-            // stable sort by w (non-negative doubles: bit order == numeric order, sign bit 0)
-            HIP_CHECK(sort_pairs(nullptr, tb, k1, k2, p2, p1, ne, 0, 63, st));
-            tmp = arena(ctx, A_SORT, tb);
-            HIP_CHECK(sort_pairs(tmp, tb, k1, k2, p2, p1, ne, 0, 63, st));
-            hipLaunchKernelGGL(edge_out_kernel, dim3(g), dim3(256), 0, st, p1, ea, eb, ew, ne, va, vb, w);
-            HIP_CHECK(hipGetLastError());
+            if (!merged) {
+                // stable sort by w (non-negative doubles: bit order == numeric order, sign bit 0)
+                HIP_CHECK(sort_pairs(nullptr, tb, k1, k2, p2, p1, ne, 0, 63, st));
+                tmp = arena(ctx, A_SORT, tb);
+                HIP_CHECK(sort_pairs(tmp, tb, k1, k2, p2, p1, ne, 0, 63, st));
+                hipLaunchKernelGGL(edge_out_kernel, dim3(g), dim3(256), 0, st, p1, ea, eb, ew, ne, va, vb, w);
+                HIP_CHECK(hipGetLastError());
+            } else {
+                // the reducers' merge order directly (SortMST.java:9-17, stable descending over
+                // FirstStep's order): the tree edges by w DESCENDING, stable over the (lo, hi)
+                // order -- exactly how a stable descending sort keeps FirstStep's (w, lo, hi)
+                // tie groups -- then merged with the self edges sorted by core (descending, ids
+                // ascending on ties), tree edges first on equal weights.  No 2n-1 re-sort.
+                HIP_CHECK(sort_pairs_desc(nullptr, tb, k1, k2, p2, p1, ne, 0, 63, st));
+                tmp = arena(ctx, A_SORT, tb);
+                HIP_CHECK(sort_pairs_desc(tmp, tb, k1, k2, p2, p1, ne, 0, 63, st));
+                if (!self_core) {
+                    hipLaunchKernelGGL(edge_out_kernel, dim3(g), dim3(256), 0, st, p1, ea, eb, ew, ne, va, vb, w);
+                    HIP_CHECK(hipGetLastError());
+                } else {
+                    auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
+                    const size_t o_tb = rnd(4 * (size_t)ne), o_tw = o_tb + rnd(4 * (size_t)ne),
+                                 o_sk = o_tw + rnd(8 * (size_t)ne), o_sk2 = o_sk + rnd(8 * (size_t)n),
+                                 o_si = o_sk2 + rnd(8 * (size_t)n), o_sp = o_si + rnd(4 * (size_t)n),
+                                 tot = o_sp + rnd(4 * (size_t)n);
+                    char *base = (char *)arena(ctx, A_WORK3, tot);
+                    int32_t *ta = (int32_t *)base, *tbv = (int32_t *)(base + o_tb);
+                    double *tw = (double *)(base + o_tw), *sk = (double *)(base + o_sk), *sk2 = (double *)(base + o_sk2);
+                    int32_t *si = (int32_t *)(base + o_si), *sperm = (int32_t *)(base + o_sp);
+                    hipLaunchKernelGGL(edge_out_kernel, dim3(g), dim3(256), 0, st, p1, ea, eb, ew, ne, ta, tbv, tw);
+                    hipLaunchKernelGGL(self_keys_kernel, dim3(g), dim3(256), 0, st, self_core, n, sk, si);
+                    size_t tb2 = 0;
+                    HIP_CHECK(sort_pairs_desc(nullptr, tb2, sk, sk2, si, sperm, n, 0, 64, st));
+                    void *tmp2 = arena(ctx, A_SORT, tb2);
+                    HIP_CHECK(sort_pairs_desc(tmp2, tb2, sk, sk2, si, sperm, n, 0, 64, st));
+                    merge_two_runs_device(ctx, ta, tbv, tw, ne, sperm, sperm, sk2, n, va, vb, w);
+                }
+            }
         }
     }
+    if (merged && self_core && n - 1 <= 0) self_edges_device(ctx, self_core, n, va, vb, w);
 }
 
 __global__ void self_edges_kernel(const double *__restrict__ core, int64_t n, int32_t *__restrict__ va,
@@ -2048,11 +2091,13 @@ static void exact_leaf_impl(hdb_ctx *ctx, const double *X, int64_t n, int min_pt
     kl.s = nb_s;
     kl.K = K;
     kl.done = done;
+    const bool self = self_edges & HDB_EDGES_SELF, merged = self_edges & HDB_EDGES_MERGED;
     {
         KernelTimer tb(ctx, "boruvka_total");
-        boruvka_on_index<D>(ctx, sp, n, extra, ctx->boruvka_knn_seed ? &kl : nullptr, va, vb, w);
+        boruvka_on_index<D>(ctx, sp, n, extra, ctx->boruvka_knn_seed ? &kl : nullptr, va, vb, w, merged,
+                            (merged && self) ? core : nullptr);
     }
-    if (self_edges) self_edges_device(ctx, core, n, va + (n - 1), vb + (n - 1), w + (n - 1));
+    if (self && !merged) self_edges_device(ctx, core, n, va + (n - 1), vb + (n - 1), w + (n - 1));
 }
 
 template <int D>
@@ -2092,7 +2137,9 @@ void exact_leaf_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int min_
     // the two calls on separate indexes (min_pts 1, tiny n, other d)
     core_distances_device(ctx, X, n, d, min_pts, metric, semantics, core);
     boruvka_device(ctx, X, n, d, core, metric, va, vb, w);
-    if (self_edges) self_edges_device(ctx, core, n, va + (n - 1), vb + (n - 1), w + (n - 1));
+    if (self_edges & HDB_EDGES_SELF) self_edges_device(ctx, core, n, va + (n - 1), vb + (n - 1), w + (n - 1));
+    if (self_edges & HDB_EDGES_MERGED)
+        sort_edges_desc_device(ctx, va, vb, w, (n - 1) + ((self_edges & HDB_EDGES_SELF) ? n : 0));
 }
 
 void boruvka_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const double *core, int metric, int32_t *va,

@@ -199,10 +199,13 @@ class HDBSCANStar:
         return UndirectedGraph(va, vb, w)
 
     def exactMST(self, dataSet, k: int, distanceFunction=None, semantics: int = A.CORE_EXCL_SELF,
-                 selfEdges: bool = True):
+                 selfEdges: bool = True, merged: bool = False):
         """FirstStep's leaf branch on one large partition (FirstStep.java:104-108):
         calculateCoreDistances + the exact MRD MST (constructMSTBoruvka's weights and edge
-        order) in one call sharing one spatial index.  Returns (core, UndirectedGraph)."""
+        order) in one call sharing one spatial index.  Returns (core, UndirectedGraph).
+        merged: the edges in the reducers' merge order (UnionFindReducer.java:19-69 +
+        SortMST.java:9-17) -- what sort_edges_desc returns for the plain list -- without the
+        re-sort (HDB_EDGES_MERGED)."""
         X = A.Arr(dataSet, np.float64)
         n, d = X.obj.shape
         ne = (n - 1) + (n if selfEdges else 0)
@@ -211,7 +214,8 @@ class HDBSCANStar:
         vb = A.new_like(X, (ne,), np.int32)
         w = A.new_like(X, (ne,), np.float64)
         c = _ctx(X, self.ctx)
-        A.check(A.lib().hdb_exact_mst(c.h, X.p, n, d, k, metric_of(distanceFunction), semantics, int(bool(selfEdges)),
+        flags = (A.EDGES_SELF if selfEdges else 0) | (A.EDGES_MERGED if merged else 0)
+        A.check(A.lib().hdb_exact_mst(c.h, X.p, n, d, k, metric_of(distanceFunction), semantics, flags,
                                       A.ptr(core), A.ptr(va), A.ptr(vb), A.ptr(w)), "exactMST")
         return core, UndirectedGraph(va, vb, w)
 

@@ -599,13 +599,15 @@ def main():
     copy_s = torch.cuda.Stream()
 
     def leaf(X):
-        _, mst = star.exactMST(X, MIN_PTS, None, pkg.CORE_EXCL_SELF, True)
+        """FirstStep's leaf (cores + exact MST + self edges), its edge list handed over in the
+        reducers' merge order (SortMST: stable descending) -- hdb_exact_mst's HDB_EDGES_MERGED,
+        identical to sorting the plain list with hdb_sort_edges_desc"""
+        _, mst = star.exactMST(X, MIN_PTS, None, pkg.CORE_EXCL_SELF, True, merged=True)
         return mst.getVerticeA(), mst.getVericeB(), mst.getEges()
 
     def merge(va, vb, w):
-        """the reducers' merge: N=1 sorts the list; N>1 sorts each rank's own list (also the
-        input of its partition's labels) and merges the presorted runs on rank 0 only"""
-        va, vb, w = pkg.sort_edges_desc(va, vb, w, ctx)
+        """the reducers' merge: N=1 the leaf's list is already in merge order; N>1 rank 0
+        merges every rank's presorted list (hdb_merge_sorted_runs)"""
         if world > 1:
             return (va, vb, w), par.gather_sorted_msts(va, vb, w, dst=0)
         return (va, vb, w), (va, vb, w)
@@ -728,8 +730,9 @@ def main():
                     try:
                         if not resident:  # the step's points uploaded from pinned host memory
                             Xw.copy_(X_pin, non_blocking=True)
-                        _, mst = st.exactMST(X_res if resident else Xw, MIN_PTS, None, pkg.CORE_EXCL_SELF, True)
-                        own = pkg.sort_edges_desc(mst.getVerticeA(), mst.getVericeB(), mst.getEges(), c)
+                        _, mst = st.exactMST(X_res if resident else Xw, MIN_PTS, None, pkg.CORE_EXCL_SELF, True,
+                                             merged=True)
+                        own = (mst.getVerticeA(), mst.getVericeB(), mst.getEges())
                         ev = torch.cuda.Event()
                         ev.record()
                         out = (ev, own)
@@ -863,7 +866,7 @@ def main():
         workers.close()
     # latency of one step without the pipeline (each step's stages back to back); its HIP
     # events time the flat labels of one partition alone
-    keys = ("knn_tree", "boruvka_total", "boruvka_scan", "merge_sort")
+    keys = ("knn_tree", "boruvka_total", "boruvka_scan")
     step_e2e()
     barrier()
     ctx.set_timing(True)
@@ -959,8 +962,9 @@ def main():
         "config": {"workload": "config 2: blobs 1M x 3 exact HDBSCAN* (no sampling), minPts 4, minClSize 4",
                    "points_per_gpu": n, "d": D, "min_pts": MIN_PTS, "min_cl_size": MIN_CL_SIZE,
                    "core": "EXCL_SELF", "timed": "X in pinned host memory -> H2D (each stage-1 worker uploads "
-                   "its step's points on its own stream) -> K1t cores -> K2b MST + self edges "
-                   "-> merge sort (N>1: per-rank sort, gather to rank 0, merge of the presorted runs) -> "
+                   "its step's points on its own stream) -> K1t cores -> K2b MST + self edges, in the merge "
+                   "order (HDB_EDGES_MERGED: tree edges sorted descending, self edges by core, one merge-path pass) "
+                   "-> N>1: gather to rank 0, merge of the presorted runs -> "
                    "K6 flat labels of the partition (D2H of the merged list overlapping it on a copy "
                    "stream) -> D2H of the labels; pipelined: step i's labels + D2H (own thread, stream and "
                    "library context) overlap step i+1's MST + merge; the timer stops after the last step's "

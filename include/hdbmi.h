@@ -164,8 +164,13 @@ int hdb_mst_boruvka(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const d
  * hdb_core_distances, bit-identical) and the exact mutual-reachability MST of
  * hdb_mst_boruvka (same weights and edge order), sharing one spatial index; the k-NN lists
  * seed every Boruvka round.  core_out nullable.  Local vertex ids 0..n-1. */
+#define HDB_EDGES_SELF 1   /* append the n self edges (HDBSCANStar.java:196-203)                  */
+#define HDB_EDGES_MERGED 2 /* return the edges in the reducers' merge order instead: exactly what
+                              hdb_sort_edges_desc returns for the plain list (UnionFindReducer.java:
+                              19-69 + SortMST.java:9-17, stable descending), without the re-sort */
 int hdb_exact_mst(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t min_pts, int32_t metric,
-                  int32_t semantics, int32_t self_edges, double *core_out, int32_t *va, int32_t *vb, double *w);
+                  int32_t semantics, int32_t self_edges /* HDB_EDGES_* flags; 0/1 as before */, double *core_out,
+                  int32_t *va, int32_t *vb, double *w);
 
 /* ---------------------------------------------------------- nearest sample (a8, a9)
  * FirstStep.call non-leaf branch (FirstStep.java:74-85): the FIRST minimum over the sample

@@ -255,3 +255,38 @@ def test_exact_mst_full_skin_weights_equal_prim(star):
     assert _spanning_tree(g.getVerticeA().cpu().numpy(), g.getVericeB().cpu().numpy(), n)
     p = star.constructMST(X, core, False)
     assert torch.equal(torch.sort(g.getEges())[0], torch.sort(p.getEges())[0])
+
+
+def _merged_vs_sorted(pkg, star, ctx, X, min_pts, self_edges=True, sem=2):
+    """hdb_exact_mst's HDB_EDGES_MERGED output must equal hdb_sort_edges_desc of its plain
+    output bit for bit (the reducers' merge order, SortMST.java:9-17, ties included)"""
+    import torch
+    Xd = torch.from_numpy(np.ascontiguousarray(X)).cuda()
+    c1, g1 = star.exactMST(Xd, min_pts, None, sem, self_edges)
+    c2, g2 = star.exactMST(Xd, min_pts, None, sem, self_edges, merged=True)
+    ref = pkg.sort_edges_desc(g1.getVerticeA(), g1.getVericeB(), g1.getEges(), ctx)
+    got = (g2.getVerticeA(), g2.getVericeB(), g2.getEges())
+    assert torch.equal(c1.view(torch.int64), c2.view(torch.int64))
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+    assert torch.equal(got[2].view(torch.int64), ref[2].view(torch.int64))
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 5, 8, 16])
+@pytest.mark.parametrize("min_pts", [2, 4, 9])
+def test_exact_mst_merged_order_equals_sort(pkg, ctx, star, d, min_pts):
+    """d 5: the two-call fallback path (re-sorted); the rest the fused leaf's merge-path order"""
+    _merged_vs_sorted(pkg, star, ctx, blobs(20000, d, 8, 3 + d), min_pts)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 64, 65, 4097])
+def test_exact_mst_merged_order_ragged_and_no_self(pkg, ctx, star, n):
+    X = blobs(n, 3, 3, n)
+    _merged_vs_sorted(pkg, star, ctx, X, 4)
+    _merged_vs_sorted(pkg, star, ctx, X, 4, self_edges=False)
+
+
+def test_exact_mst_merged_order_ties_full_size(pkg, ctx, star):
+    """Skin (heavy duplication: huge zero-weight tie groups between tree and self edges) and
+    1M blobs (the bench's partition)"""
+    _merged_vs_sorted(pkg, star, ctx, load_skin(), 4)
+    _merged_vs_sorted(pkg, star, ctx, blobs(1_000_000, 3, 20, 1), 4)
