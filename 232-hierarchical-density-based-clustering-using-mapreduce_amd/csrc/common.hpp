@@ -80,7 +80,9 @@ struct hdb_ctx {
     bool prim_coop_plain = true;   // launch it as a plain kernel first (cooperative launches serialise)
     bool bubble_knn_split = true;  // K5: candidate range in chunks + merge (one thread per bubble is 256 waves at 16k)
     bool prim_coop_xcd = true;     // plain attempt: working blocks on one XCD exchange through its L2 (checked at run time)
-    int prim_coop_xcd_max_wg = 32;  // ... for Prims of at most this many 1024-thread workgroups
+    int prim_coop_xcd_max_wg = 32;  // ... for Prims of at most this many workgroups (one XCD: 32 CUs)
+    int prim_coop_bs = 1024;  // cooperative Prim (slots 4/5) workgroup size; 0: the smallest of 128..1024 that keeps
+                              // the Prim within prim_coop_xcd_max_wg workgroups (more CUs share a step's relaxation)
     int prim_coop_plain_spin_log2 = 20;  // plain attempt: polls per exchange before it reports non-co-residency
     int prim_coop_slots = 4;  // cooperative Prim exchange, rows in registers (d <= 16): 1 release/acquire slots, 2 granules,
                               // 3 drained sc1 slots, 4 DPP folds + key granules (default), 5 key+row granule sweep

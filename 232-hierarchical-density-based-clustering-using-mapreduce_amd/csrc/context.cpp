@@ -168,6 +168,7 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         if (const char *e = getenv("HDB_PRIM_XCD")) c->prim_coop_xcd = atoi(e) != 0;       // A/B knob
         if (const char *e = getenv("HDB_BUBBLE_SPLIT")) c->bubble_knn_split = atoi(e) != 0;  // A/B knob
         if (const char *e = getenv("HDB_PRIM_XCD_MAX_WG")) c->prim_coop_xcd_max_wg = atoi(e);  // A/B knob
+        if (const char *e = getenv("HDB_PRIM_COOP_BS")) c->prim_coop_bs = atoi(e);             // A/B knob
         if (const char *e = getenv("HDB_FLAT_LINK")) c->flat_link_variant = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_FLAT_ROOT")) c->flat_root_variant = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_MERGE_RUNS")) c->merge_runs = atoi(e) != 0;      // A/B knob
@@ -304,6 +305,11 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
     }
     if (k == "prim_coop") {
         ctx->prim_coop = value != 0;
+        return HDB_OK;
+    }
+    if (k == "prim_coop_bs") {
+        if (value != 0 && value != 128 && value != 256 && value != 512 && value != 1024) return HDB_EINVAL;
+        ctx->prim_coop_bs = (int)value;
         return HDB_OK;
     }
     if (k == "prim_coop_slots") {

@@ -1115,10 +1115,9 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
     }
 }
 
-template <int DM, bool FULL>
-static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
-                         int32_t *va, int32_t *vb, double *w) {
-    constexpr int BS = 1024;
+template <int DM, bool FULL, int BS>
+static bool launch_coop4_bs(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
+                            int32_t *va, int32_t *vb, double *w) {
     const int nwg = (int)ceil_div(n, BS);
     if (nwg > 64) return false;
     int coop = 0, ncu = 0, per_cu = 0;
@@ -1187,6 +1186,29 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
     }
     HDB_THROW(HDB_EDEVICE, "prim_coop: key sweep timed out (workgroups not co-resident)");
     return true;
+}
+
+// workgroup size: 1024 by default; prim_coop_bs = 0 takes the smallest of 128..1024 that keeps
+// the Prim within prim_coop_xcd_max_wg workgroups (one XCD), so more CUs -- and fewer waves per
+// SIMD -- share each step's relaxation
+template <int DM, bool FULL>
+static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
+                         int32_t *va, int32_t *vb, double *w) {
+    int bs = ctx->prim_coop_bs;
+    if (bs == 0) {
+        bs = 1024;
+        for (int b = 128; b < 1024; b *= 2)
+            if (ceil_div(n, (int64_t)b) <= ctx->prim_coop_xcd_max_wg) {
+                bs = b;
+                break;
+            }
+    }
+    switch (bs) {
+    case 128: return launch_coop4_bs<DM, FULL, 128>(ctx, in, o, n, eo, self_edges, va, vb, w);
+    case 256: return launch_coop4_bs<DM, FULL, 256>(ctx, in, o, n, eo, self_edges, va, vb, w);
+    case 512: return launch_coop4_bs<DM, FULL, 512>(ctx, in, o, n, eo, self_edges, va, vb, w);
+    default: return launch_coop4_bs<DM, FULL, 1024>(ctx, in, o, n, eo, self_edges, va, vb, w);
+    }
 }
 
 template <int DM, bool FAST>
