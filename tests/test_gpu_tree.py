@@ -271,10 +271,10 @@ def _merged_vs_sorted(pkg, star, ctx, X, min_pts, self_edges=True, sem=2):
     assert torch.equal(got[2].view(torch.int64), ref[2].view(torch.int64))
 
 
-@pytest.mark.parametrize("d", [1, 2, 3, 5, 8, 16])
-@pytest.mark.parametrize("min_pts", [2, 4, 9])
+@pytest.mark.parametrize("d", [1, 2, 3, 4, 8, 16])
+@pytest.mark.parametrize("min_pts", [1, 2, 4, 9])
 def test_exact_mst_merged_order_equals_sort(pkg, ctx, star, d, min_pts):
-    """d 5: the two-call fallback path (re-sorted); the rest the fused leaf's merge-path order"""
+    """minPts 1: the two-call fallback path (re-sorted); the rest the fused leaf's merge-path order"""
     _merged_vs_sorted(pkg, star, ctx, blobs(20000, d, 8, 3 + d), min_pts)
 
 
