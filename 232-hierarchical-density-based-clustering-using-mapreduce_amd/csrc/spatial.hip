@@ -493,6 +493,9 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
     }
 }
 
+#ifndef HDB_BOR_TWOPASS
+#define HDB_BOR_TWOPASS 1  // K2b leaf groups: distances first (independent), exact updates on the hits only
+#endif
 #ifndef HDB_BOR_PROF
 #define HDB_BOR_PROF 0  // diagnostic build: per-wave cycle split of the K2b scan (stats boruvka_prof_*)
 #endif
@@ -935,7 +938,54 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
             const bool need = gneeds(gi);  // re-test in registers: the bound may have tightened
             if (!__any(need)) continue;
             const int q0 = gi * SG;
-            const int q1 = (int)min<int64_t>(SG, n - (idx * BT + q0)) + q0;
+            const int nq = (int)min<int64_t>(SG, n - (idx * BT + q0));
+#if HDB_BOR_TWOPASS
+            // Pass 1: the group's squared distances against the bound at the group's start --
+            // independent candidates, so their LDS reads and FP64 chains overlap (the one-pass
+            // loop carried the lane's best from candidate to candidate: a dependent chain of
+            // ~200 cycles per candidate at the 1-3 waves per SIMD of the early rounds).  The
+            // bound only tightens, so a candidate failing it here fails it at its turn too.
+            const double sb0 = sb;
+            unsigned hit = 0;
+#pragma unroll 8
+            for (int k = 0; k < SG; k++) {
+                const LRec<D> r = cand[q0 + k];  // uniform address -> LDS broadcast
+                double s = sq_diff(mx[0], r.x[0]);
+#pragma unroll
+                for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
+                const bool ok = need & (k < nq) & (r.comp != mcomp);
+                if (STATS) nev += ok ? 1 : 0;  // pair evaluated for a lane that needs it
+                hit |= (ok & (s <= sb0)) ? (1u << k) : 0u;  // (s <= sb0) also drops NaN
+            }
+            unsigned any_hit = hit;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) any_hit |= __shfl_xor(any_hit, o);
+            any_hit = __builtin_amdgcn_readfirstlane(any_hit);
+            // Pass 2: the exact sequential update over the hits, in candidate order (the same
+            // sequence of best edges as the one-pass loop)
+#pragma unroll 1
+            while (any_hit) {
+                const int k = __builtin_ctz(any_hit);
+                any_hit &= any_hit - 1;
+                if (!((hit >> k) & 1u)) continue;
+                const LRec<D> r = cand[q0 + k];
+                double s = sq_diff(mx[0], r.x[0]);  // recomputed: bit-identical
+#pragma unroll
+                for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
+                if (!(s <= sb)) continue;
+                double mrd = sqrt(s);  // HDBSCANStar.java:162-168 order
+                if (mcore > mrd) mrd = mcore;
+                if (r.core > mrd) mrd = r.core;
+                const int32_t lo = mid < r.id ? mid : r.id;
+                const int32_t hi = mid < r.id ? r.id : mid;
+                if (key_less(mrd, s, lo, hi, b)) {
+                    b = Best{mrd, s, lo, hi};
+                    sb = own_sb();
+                    found = true;
+                }
+            }
+#else
+            const int q1 = q0 + nq;
 #pragma unroll CAND_UNROLL
             for (int qq = q0; qq < q1; qq++) {
                 const LRec<D> r = cand[qq];  // uniform address -> LDS broadcast
@@ -956,6 +1006,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
                     found = true;
                 }
             }
+#endif
         }
         prof.mark(7);
         if (found) {
@@ -1491,6 +1542,38 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
             if (j1 <= j0) break;
             nev += (unsigned long long)(j1 - j0);
             const int q0 = gi * SG, q1 = q0 + (int)(j1 - j0);
+#if HDB_BOR_TWOPASS
+            // Pass 1: the group's distances against the K-th value at the group's start
+            // (independent candidates: their LDS reads and FP64 chains overlap; the K-th value
+            // only falls, so a candidate failing here is skipped by the insertion test too).
+            // Pass 2: insertions of the hits in candidate order (the same list, ties included).
+            const double thr0 = buf[K - 1];
+            unsigned hit = 0;
+#pragma unroll 8
+            for (int k = 0; k < SG; k++) {
+                const LRec<D> r = cand[q0 + k];  // uniform address -> LDS broadcast
+                double s = sq_diff(mx[0], r.x[0]);
+#pragma unroll
+                for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
+                hit |= ((q0 + k < q1) & (r.id != skip_self) & (s < thr0)) ? (1u << k) : 0u;
+            }
+            unsigned any_hit = hit;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) any_hit |= __shfl_xor(any_hit, o);
+            any_hit = __builtin_amdgcn_readfirstlane(any_hit);
+#pragma unroll 1
+            while (any_hit) {
+                const int k = __builtin_ctz(any_hit);
+                any_hit &= any_hit - 1;
+                if (!((hit >> k) & 1u)) continue;
+                const LRec<D> r = cand[q0 + k];
+                double s = sq_diff(mx[0], r.x[0]);  // recomputed: bit-identical
+#pragma unroll
+                for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
+                if (IDX) topk_insert_idx<K>(buf, bix, s, (int)(tile * BT + q0 + k));
+                else topk_insert<K>(buf, s);
+            }
+#else
 #pragma unroll CAND_UNROLL
             for (int qq = q0; qq < q1; qq++) {
                 const LRec<D> r = cand[qq];  // uniform address -> LDS broadcast
@@ -1501,6 +1584,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
                 if (IDX) topk_insert_idx<K>(buf, bix, s, (int)(tile * BT + qq));
                 else topk_insert<K>(buf, s);
             }
+#endif
         }
     };
     scan_leaf(t, true);  // own tile first: the K-th bound is tight from the start
