@@ -516,6 +516,15 @@ __device__ __forceinline__ double coop_mrd(const PrimIn &in, const double (&xc)[
                 improves = false;
                 return best;
             }
+        } else {
+            // bubbles: with E = eB_c + eB_i >= 0 and nnB_c + nnB_i >= 0, distanceBubbles(d) >=
+            // fl(d - E) > best once d > (best + E)(1 + 1e-12) (the margin covers every rounding
+            // of sqrt, the subtraction and the square): no improvement, skip the sqrt
+            const double E = ebc + ebi, T = (best + E) * (1.0 + 1e-12);
+            if (s > T * T && E >= 0.0 && nnc + nni >= 0.0) {
+                improves = false;
+                return best;
+            }
         }
         dist = sqrt(s);
     } else {
@@ -985,8 +994,10 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
             }
             key = mrd_key(best);
         }
+        COOP_T(6);
         const unsigned long long wmin = wave_min_u64(key);
         const int wl = last_lane(key == wmin);
+        COOP_T(7);
         if (lane == wl) {  // the wave's candidate parks its row
 #pragma unroll
             for (int c = 0; c < DM; c++) s_cand[wid][c] = xi[c];

@@ -24,11 +24,19 @@ ctx = pkg.Context.get(0)
 ctx.use_torch_stream()
 star = pkg.HDBSCANStar(ctx)
 ctx.set_option("prim_coop_slots", int(os.environ.get("SLOTS", "4")))
-star.constructMST(X, core, True, None, ids)
+if os.environ.get("BUBBLES"):
+    rngb = np.random.default_rng(1)
+    eB = torch.from_numpy(np.abs(rngb.normal(0.3, 0.1, n))).cuda()
+    nnB = torch.from_numpy(np.abs(rngb.normal(0.2, 0.05, n))).cuda()
+    nB = torch.from_numpy(rngb.integers(1, 9, n).astype(np.int32)).cuda()
+    pkg.HdbscanDataBubbles(ctx).constructMSTBubbles(X, nB, eB, nnB, ids, core, True)
+else:
+    star.constructMST(X, core, True, None, ids)
 torch.cuda.synchronize()
 buf = (C.c_ulonglong * 512)()
 A.lib().hdb_debug_coop_prof(buf)
-t = np.array(buf, dtype=np.int64).reshape(64, 8)[:, :6]
+t8 = np.array(buf, dtype=np.int64).reshape(64, 8)
+t = t8[:, :6]
 names = ["mrd+wave reduce+sync", "fold+publish", "poll (tags)", "fold+row load", "final sync", "-> next step"]
 dif = np.diff(t, axis=1)
 nxt = t[1:, 0] - t[:-1, 5]
@@ -36,3 +44,7 @@ print(f"n={n} d={d} cycles/step median {np.median(t[1:, 0] - t[:-1, 0]):.0f}")
 for j in range(5):
     print(f"  {names[j]:22s} median {np.median(dif[:, j]):7.0f}  p90 {np.percentile(dif[:, j], 90):7.0f}")
 print(f"  {names[5]:22s} median {np.median(nxt):7.0f}")
+if np.any(t8[:, 6]):  # slots 4/5 kernels: relaxation / wave minimum split of phase 0
+    print(f"    relax (mrd + key)      median {np.median(t8[:, 6] - t8[:, 0]):7.0f}")
+    print(f"    wave min + last lane   median {np.median(t8[:, 7] - t8[:, 6]):7.0f}")
+    print(f"    park + barrier         median {np.median(t8[:, 1] - t8[:, 7]):7.0f}")

@@ -6,4 +6,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_tree.py tests/test_gpu_pari
 HDBMI_LIB=$PWD/ab/borprof/libhdbmi.so timeout -k 10 200 python -u tools/boruvka_stats.py > $OUT/borprof.log 2>&1 || { echo "borprof failed"; tail -20 $OUT/borprof.log; exit 1; }
 timeout -k 10 900 bash tools/ab_c2.sh onepass > $OUT/ab_c2.log 2>&1 || { echo "ab failed"; tail -20 $OUT/ab_c2.log; exit 1; }
 timeout -k 10 300 python -u bench.py > $OUT/bench_c2.json.log 2>&1 || { echo "bench c2 failed"; tail -20 $OUT/bench_c2.json.log; exit 1; }
+HDBMI_LIB=$PWD/ab/coopprof/libhdbmi.so timeout -k 10 120 python -u tools/coop_prof.py 16384 8 > $OUT/coopprof.log 2>&1 || { echo "coopprof failed"; exit 1; }
+BUBBLES=1 HDBMI_LIB=$PWD/ab/coopprof/libhdbmi.so timeout -k 10 120 python -u tools/coop_prof.py 16384 8 > $OUT/coopprof_bubbles.log 2>&1 || { echo "coopprof b failed"; exit 1; }
+timeout -k 10 120 python -u tools/prim_xcd_bench.py 16384 8 > $OUT/prim16k.log 2>&1 || { echo "prim bench failed"; exit 1; }
 echo done
