@@ -901,6 +901,9 @@ static bool launch_coop3(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
 // line stays in that XCD's L2, which every CU's sc1 poll reads) instead of sc1 stores (which
 // drop the line from L2, so every poll crossed the fabric).  Any other placement keeps the sc1
 // protocol: placement changes only speed.
+#ifndef HDB_COOP_CACHE
+#define HDB_COOP_CACHE 1
+#endif
 template <int BS, int DM, bool FULL>
 __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int self_edges, int32_t *__restrict__ va,
                                                         int32_t *__restrict__ vb, double *__restrict__ w,
@@ -982,48 +985,66 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
     }
     int cur = n - 1;
     constexpr unsigned long long KINF = 0x7ff0000000000000ull;  // key of +inf: nothing to offer
+    // Candidate caching (HDB_COOP_CACHE): a wave's candidate changes only when one of its lanes
+    // improved or its parked winner was attached in the last step, and a workgroup's only when
+    // one of its waves' did -- most steps relax nothing near most waves (the sqrt-free rejection
+    // in coop_mrd), so the wave minimum, the parking and the workgroup fold are skipped and the
+    // workgroup republishes its cached granule values under the new step's tag.
+    __shared__ int s_dirty;
+    if (tid == 0) s_dirty = 0;
+    bool just = false;    // this lane was attached at the end of the last step
+    unsigned val_c = 0u;  // wave 0: the workgroup's cached granule value (this lane's)
     for (int step = 1; step < n; step++) {
         COOP_T(0);
-        unsigned long long key = KINF;
-        if (!att) {
-            bool imp;
-            const double mrd = coop_mrd<DM>(in, xc, cc, ebc, nnc, xi, ci, ebi, nni, best, imp);
-            if (imp) {
-                best = mrd;
-                par = cur;
-            }
-            key = mrd_key(best);
+        bool imp = false;
+        double mrd = 0.0;
+        if (!att) mrd = coop_mrd<DM>(in, xc, cc, ebc, nnc, xi, ci, ebi, nni, best, imp);
+        if (imp) {
+            best = mrd;
+            par = cur;
         }
         COOP_T(6);
-        const unsigned long long wmin = wave_min_u64(key);
-        const int wl = last_lane(key == wmin);
-        COOP_T(7);
-        if (lane == wl) {  // the wave's candidate parks its row
+        const bool dirty = !HDB_COOP_CACHE || step == 1 || __any(imp || just);
+        just = false;
+        if (dirty) {
+            const unsigned long long key = att ? KINF : mrd_key(best);
+            const unsigned long long wmin = wave_min_u64(key);
+            const int wl = last_lane(key == wmin);
+            if (lane == wl) {  // the wave's candidate parks its row
 #pragma unroll
-            for (int c = 0; c < DM; c++) s_cand[wid][c] = xi[c];
-            s_cand[wid][DM] = ci;
-            s_cand[wid][DM + 1] = ebi;
-            s_cand[wid][DM + 2] = nni;
-            s_cand[wid][ND] = best;
-            s_ci[wid] = wmin < KINF ? i : -1;
+                for (int c = 0; c < DM; c++) s_cand[wid][c] = xi[c];
+                s_cand[wid][DM] = ci;
+                s_cand[wid][DM + 1] = ebi;
+                s_cand[wid][DM + 2] = nni;
+                s_cand[wid][ND] = best;
+                s_ci[wid] = wmin < KINF ? i : -1;
+                s_dirty = 1;
+            }
         }
+        COOP_T(7);
         __syncthreads();
         COOP_T(1);
         if (wid == 0) {
             const int buf = step & 1;
             const unsigned tag = (unsigned)step;
-            // fold the waves: lane q holds wave q's candidate
-            const int qi = lane < NW ? s_ci[lane] : -1;
-            const unsigned long long qk = qi >= 0 ? mrd_key(s_cand[lane < NW ? lane : 0][ND]) : KINF;
-            const unsigned long long gmin = wave_min_u64(qk);
-            const int q = min(last_lane(qk == gmin), NW - 1);  // all waves empty: any wave (index -1)
-            const unsigned *cw = (const unsigned *)s_cand[q];
-            const int gidx = __shfl(qi, q);
-            // publish: lanes 0-2 the key granules, lanes 3 .. 3 + 2 ND the row granules
             unsigned val;
-            if (lane < 2) val = cw[2 * ND + lane];
-            else if (lane == 2) val = (unsigned)gidx;
-            else val = lane < 3 + 2 * ND ? cw[lane - 3] : 0u;
+            if (!HDB_COOP_CACHE || s_dirty) {
+                // fold the waves: lane q holds wave q's candidate
+                const int qi = lane < NW ? s_ci[lane] : -1;
+                const unsigned long long qk = qi >= 0 ? mrd_key(s_cand[lane < NW ? lane : 0][ND]) : KINF;
+                const unsigned long long gmin = wave_min_u64(qk);
+                const int q = min(last_lane(qk == gmin), NW - 1);  // all waves empty: any wave (index -1)
+                const unsigned *cw = (const unsigned *)s_cand[q];
+                const int gidx = __shfl(qi, q);
+                // publish: lanes 0-2 the key granules, lanes 3 .. 3 + 2 ND the row granules
+                if (lane < 2) val = cw[2 * ND + lane];
+                else if (lane == 2) val = (unsigned)gidx;
+                else val = lane < 3 + 2 * ND ? cw[lane - 3] : 0u;
+                val_c = val;
+            } else
+                val = val_c;
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) s_dirty = 0;  // every lane of wave 0 has read it; set again only after the next barrier
             const unsigned long long gv = ((unsigned long long)tag << 32) | val;
             gu64 *dst = nullptr;
             if (FULL) {
@@ -1112,7 +1133,10 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
         cc = s_row[DM];
         ebc = s_row[DM + 1];
         nnc = s_row[DM + 2];
-        if (i == cur) att = true;
+        if (i == cur) {
+            att = true;
+            just = true;
+        }
     }
     if (i < n - 1) {
         va[i] = par >= 0 ? in.ids[par] : 0;

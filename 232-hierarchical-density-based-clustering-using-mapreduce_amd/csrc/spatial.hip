@@ -493,6 +493,12 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
     }
 }
 
+#ifndef HDB_BOR_REFRESH_LOG2
+#define HDB_BOR_REFRESH_LOG2 3  // K2b: re-read the component bound every 2^x node visits
+#endif
+#ifndef HDB_BOR_LEAF_PUBLISH
+#define HDB_BOR_LEAF_PUBLISH 1  // K2b: publish a lane's better edge to the component bound at once
+#endif
 #ifndef HDB_BOR_TWOPASS
 #define HDB_BOR_TWOPASS 1  // K2b leaf groups: distances first (independent), exact updates on the hits only
 #endif
@@ -867,7 +873,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
         const int lev = code >> 26;
         const int64_t idx = code & ((1 << 26) - 1);
         const int64_t node = off_s[lev] + idx;
-        if ((visits++ & 7) == 0) refresh();
+        if ((visits++ & ((1 << HDB_BOR_REFRESH_LOG2) - 1)) == 0) refresh();
         prof.mark(1);
         // re-test the popped node with the current bound (its parent tested it when pushing)
         if (pop_test & 1) {
@@ -1013,7 +1019,8 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
             const double c2 = (b.w * b.w) * (1.0 + 1e-12);
             if (c2 < cb2) {
                 const unsigned long long bw = (unsigned long long)dbits(b.w);
-                if (bw < __hip_atomic_load(&comp_w[mcomp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                if (HDB_BOR_LEAF_PUBLISH &&
+                    bw < __hip_atomic_load(&comp_w[mcomp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                     atomicMin(&comp_w[mcomp], bw);
                 cb2 = c2;
                 if (b.w < cwv) cwv = b.w;
