@@ -32,6 +32,82 @@ __global__ void bubble_count_kernel(const int32_t *__restrict__ bo, int64_t n, i
     }
 }
 
+// K4 fold, one lane per (bubble, dimension): a coordinate's LS and SS are two independent
+// sequential chains over the bubble's members (ascending id, D5), kept in registers -- the same
+// additions in the same order as the per-bubble fold, bit for bit.  nb x d lanes instead of nb
+// (16,384 bubbles: 256 waves -> 2,048 at d = 8), and no read-modify-write of the outputs per
+// member.  The epilogue (rep, extent, nnDist: sequential over dimensions) runs per bubble after.
+__global__ void bubble_fold_dim_kernel(const double *__restrict__ X, int d, const int32_t *__restrict__ perm,
+                                       const int64_t *__restrict__ off, int64_t nb, double *__restrict__ ls,
+                                       double *__restrict__ ss) {
+    HDB_GRID_STRIDE(t, nb * d) {
+        const int64_t b = t / d;
+        const int c = (int)(t - b * d);
+        const int64_t lo = off[b], hi = off[b + 1];
+        double L = 0.0, Q = 0.0;
+        if (lo < hi) {
+            const double v0 = X[(int64_t)perm[lo] * d + c];
+            L = v0;
+            Q = v0 * v0;
+#pragma unroll 4
+            for (int64_t k = lo + 1; k < hi; k++) {
+                const double v = X[(int64_t)perm[k] * d + c];
+                L = L + v;
+                Q = Q + (v * v);
+            }
+        }
+        ls[t] = L;
+        ss[t] = Q;
+    }
+}
+
+// per-bubble epilogue of the folded (LS, SS, n): exactly the tail of bubble_fold_kernel
+__global__ void bubble_epilogue_kernel(int d, const int64_t *__restrict__ off, int64_t nb, int variant,
+                                       const double *__restrict__ ls, const double *__restrict__ ss,
+                                       double *__restrict__ rep, double *__restrict__ info) {
+    HDB_GRID_STRIDE(b, nb) {
+        const int64_t cnt = off[b + 1] - off[b];
+        const double *L = ls + b * d, *Q = ss + b * d;
+        double *R = rep + b * d, *I = info + b * 3;
+        if (cnt == 0) {
+            for (int c = 0; c < d; c++) R[c] = 0;
+            I[0] = I[1] = I[2] = 0;
+            continue;
+        }
+        if (cnt == 1) {
+            for (int c = 0; c < d; c++) R[c] = L[c];  // rep = ls (FirstStep.java:100)
+            I[0] = 0;
+            I[1] = 0;
+            I[2] = 1;
+            continue;
+        }
+        if (variant == HDB_BUBBLE_COMBINESTEP) {
+            const double n = (double)cnt;  // n += 1 per call == member count (sequential fold)
+            for (int c = 0; c < d; c++) R[c] = L[c] / n;  // computeRepBubble (:58-64)
+            double extent = 0.0;                          // computeExtentBubble (:46-56)
+            for (int c = 0; c < d; c++) {
+                double v = ((2 * n * Q[c]) - (2 * (L[c] * L[c])));
+                if (v >= 0) extent += sqrt(v / (n * (n - 1)));
+            }
+            extent = extent / d;
+            I[0] = extent;
+            // computeNNDistBubble (:42-44): pow(1/n, (int)(1/d)) * extent
+            I[1] = pow((1 / n), (double)(1 / d)) * extent;
+            I[2] = n;
+        } else {
+            const int32_t n = (int32_t)cnt;
+            for (int c = 0; c < d; c++) R[c] = L[c] / n;
+            const int32_t prod = (int32_t)((uint32_t)n * (uint32_t)(n - 1));  // Java int overflow
+            double sum = 0.0;
+            for (int c = 0; c < d; c++) sum = sum + (((2 * n * Q[c]) - (2 * (L[c] * L[c]))) / prod);
+            const double extent = sqrt(sum);
+            I[0] = extent;
+            I[1] = pow((double)1 / n, (double)1 / d) * extent;
+            I[2] = n;
+        }
+    }
+}
+
 // one lane per bubble: sequential fold in member order
 __global__ void bubble_fold_kernel(const double *__restrict__ X, int d, const int32_t *__restrict__ perm,
                                    const int64_t *__restrict__ off, int64_t nb, int variant,
@@ -133,8 +209,14 @@ void bubble_stats_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const 
         void *tmp = arena(ctx, A_SORT, tb);
         HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, offs, (int)(nb + 1), ctx->stream));
     }
-    hipLaunchKernelGGL(bubble_fold_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(nb, 64), 4096)), dim3(64), 0,
-                       ctx->stream, X, d, perm, offs, nb, variant, ls, ss, rep, info);
+    if (ctx->bubble_fold_dim) {
+        hipLaunchKernelGGL(bubble_fold_dim_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(nb * d, 256), 16384)),
+                           dim3(256), 0, ctx->stream, X, d, perm, offs, nb, ls, ss);
+        hipLaunchKernelGGL(bubble_epilogue_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(nb, 64), 4096)), dim3(64),
+                           0, ctx->stream, d, offs, nb, variant, ls, ss, rep, info);
+    } else
+        hipLaunchKernelGGL(bubble_fold_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(nb, 64), 4096)), dim3(64), 0,
+                           ctx->stream, X, d, perm, offs, nb, variant, ls, ss, rep, info);
     HIP_CHECK(hipGetLastError());
     int h_bad = 0;
     HIP_CHECK(hipMemcpyAsync(&h_bad, bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));

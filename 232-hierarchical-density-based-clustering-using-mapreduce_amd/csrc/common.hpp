@@ -78,6 +78,7 @@ struct hdb_ctx {
     int trav_pop_test = 0;         // bit 0: Boruvka re-tests a popped node, bit 1: K1t a popped leaf
     bool prim_coop = true;         // cooperative single-launch Prim for 4096 < n <= 65536
     bool prim_coop_plain = true;   // launch it as a plain kernel first (cooperative launches serialise)
+    bool bubble_fold_dim = true;   // K4: one lane per (bubble, dimension) fold (0: one lane per bubble, A/B)
     bool bubble_knn_split = true;  // K5: candidate range in chunks + merge (one thread per bubble is 256 waves at 16k)
     bool prim_coop_xcd = true;     // plain attempt: working blocks on one XCD exchange through its L2 (checked at run time)
     int prim_coop_xcd_max_wg = 32;  // ... for Prims of at most this many workgroups (one XCD: 32 CUs)

@@ -290,6 +290,10 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
         ctx->prim_coop_plain = value != 0;
         return HDB_OK;
     }
+    if (k == "bubble_fold_dim") {
+        ctx->bubble_fold_dim = value != 0;
+        return HDB_OK;
+    }
     if (k == "bubble_knn_split") {
         ctx->bubble_knn_split = value != 0;
         return HDB_OK;
