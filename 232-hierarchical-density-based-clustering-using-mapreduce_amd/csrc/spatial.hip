@@ -511,7 +511,11 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
 // 5 leaf record/group-box staging, 6 leaf group mask, 7 leaf candidate loops, 8 bound publish,
 // 9 tail (best writes, component minimum).
 constexpr int BOR_PROF_N = 10;
-constexpr int BOR_STATS_HDR = 32;  // stats: [0..4] sums, [16..25] cycle split, then one word per wave
+// STATS: one record of BOR_STATS_REC words per wave (no same-address atomics: thousands of waves
+// adding into one line serialise at its L2 channel and slow every load that maps there):
+// [0] pair evals, [1] leaves, [2] visits, [3] lanes searching at start, [4] any such lane,
+// [5] shader cycles, [6..15] cycle split (HDB_BOR_PROF); summed on the host
+constexpr int BOR_STATS_REC = 16;
 template <bool ON>
 struct BorProf {
     unsigned long long pc[BOR_PROF_N];
@@ -1049,15 +1053,16 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
         for (int off = 32; off >= 1; off >>= 1) nev += __shfl_xor(nev, off);
         const unsigned long long act_mask = __ballot(active0);
         if (lane == 0) {
-            atomicAdd(&stats[0], nev);
-            atomicAdd(&stats[1], n_leaf);
-            atomicAdd(&stats[2], (unsigned long long)visits);
-            atomicAdd(&stats[3], (unsigned long long)__popcll(act_mask));  // lanes searching at start
-            atomicAdd(&stats[4], (unsigned long long)(act_mask != 0));     // waves with any such lane
+            unsigned long long *rec = stats + (size_t)t * BOR_STATS_REC;
+            rec[0] = nev;
+            rec[1] = n_leaf;
+            rec[2] = (unsigned long long)visits;
+            rec[3] = (unsigned long long)__popcll(act_mask);  // lanes searching at start
+            rec[4] = (unsigned long long)(act_mask != 0);     // waves with any such lane
 #if HDB_BOR_PROF
-            for (int k = 0; k < BOR_PROF_N; k++) atomicAdd(&stats[16 + k], prof.pc[k]);
+            for (int k = 0; k < BOR_PROF_N; k++) rec[6 + k] = prof.pc[k];
 #endif
-            stats[BOR_STATS_HDR + t] = (unsigned long long)(clock64() - t_start);  // per-wave shader cycles
+            rec[5] = (unsigned long long)(clock64() - t_start);  // per-wave shader cycles
         }
     }
 }
@@ -1903,7 +1908,7 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
     int32_t *gcnt = ex.take<int32_t>(ngroups), *gwaves = ex.take<int32_t>(ngroups), *woff = ex.take<int32_t>(ngroups);
     unsigned long long *desc = ex.take<unsigned long long>(max_waves);
     int32_t *nwaves = ex.take<int32_t>(1);
-    unsigned long long *evals = ctx->count_evals ? ex.take<unsigned long long>(BOR_STATS_HDR + max_waves) : nullptr;
+    unsigned long long *evals = ctx->count_evals ? ex.take<unsigned long long>((size_t)BOR_STATS_REC * max_waves) : nullptr;
     int64_t tot_evals = 0;
     Rec<D> *recs = sp.recs;
     int32_t *inv = sp.inv;
@@ -1976,7 +1981,7 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
                            tcomp + bvh.off[1], n_inner);
         hipLaunchKernelGGL(retag_kernel<D>, dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, st, recs, pcomp, n,
                            ntiles, bvh.levels, round > 0 ? parent2 : nullptr, tcomp, bvh.stag);
-        if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 8 * (BOR_STATS_HDR + max_waves), st));
+        if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 8 * (size_t)BOR_STATS_REC * max_waves, st));
         round_seed(round);
         {
             KernelTimer ts(ctx, "boruvka_scan");
@@ -2000,19 +2005,22 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
                                    nwaves, ctx->trav_pop_test, inv, best_pos, n_edges, bs.lbw, bs.xact, evals);
         }
         if (evals) {
-            unsigned long long h[BOR_STATS_HDR];
-            HIP_CHECK(hipMemcpyAsync(h, evals, 8 * BOR_STATS_HDR, hipMemcpyDeviceToHost, st));
+            std::vector<unsigned long long> recs_h((size_t)BOR_STATS_REC * max_waves);
+            HIP_CHECK(hipMemcpyAsync(recs_h.data(), evals, 8 * recs_h.size(), hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
+            unsigned long long h[BOR_STATS_REC] = {};
+            wave_cyc.clear();
+            for (int64_t t = 0; t < max_waves; t++) {
+                const unsigned long long *rec = recs_h.data() + (size_t)t * BOR_STATS_REC;
+                for (int k = 0; k < BOR_STATS_REC; k++) h[k] += rec[k];
+                if (rec[5]) wave_cyc.push_back(rec[5]);  // waves that ran (exited waves leave 0)
+            }
             const std::string r = "boruvka_r" + std::to_string(round);
             if (HDB_BOR_PROF) {
                 static const char *pn[BOR_PROF_N] = {"setup", "pop", "stage", "test", "push",
                                                      "leaf_load", "leaf_mask", "leaf_eval", "publish", "tail"};
-                for (int k = 0; k < BOR_PROF_N; k++) ctx->stats[r + "_prof_" + pn[k]] = (int64_t)h[16 + k];
+                for (int k = 0; k < BOR_PROF_N; k++) ctx->stats[r + "_prof_" + pn[k]] = (int64_t)h[6 + k];
             }
-            wave_cyc.resize(max_waves);
-            HIP_CHECK(hipMemcpyAsync(wave_cyc.data(), evals + BOR_STATS_HDR, 8 * max_waves, hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-            wave_cyc.erase(std::remove(wave_cyc.begin(), wave_cyc.end(), 0ull), wave_cyc.end());  // exited waves
             if (wave_cyc.empty()) wave_cyc.push_back(0);
             std::sort(wave_cyc.begin(), wave_cyc.end());
             unsigned long long cs = 0;
