@@ -497,10 +497,10 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
 #define HDB_BOR_REFRESH_LOG2 3  // K2b: re-read the component bound every 2^x node visits
 #endif
 #ifndef HDB_BOR_LEAF_PUBLISH
-#define HDB_BOR_LEAF_PUBLISH 1  // K2b: publish a lane's better edge to the component bound at once
+#define HDB_BOR_LEAF_PUBLISH 0  // K2b: publish a better edge to the component bound at once (A/B r04: the same-address atomics cost more than the pruning they buy, scan 4.35 -> 3.90 ms; the wave tail still publishes)
 #endif
 #ifndef HDB_BOR_TWOPASS
-#define HDB_BOR_TWOPASS 1  // K2b leaf groups: distances first (independent), exact updates on the hits only
+#define HDB_BOR_TWOPASS 0  // K2b/K1t leaf groups: distances first, exact updates on the hits only (A/B r04: slower -- K1t 2.05 -> 2.28 ms, scan +0.15 ms: the loop is VALU-issue bound, not a dependent chain)
 #endif
 #ifndef HDB_BOR_PROF
 #define HDB_BOR_PROF 0  // diagnostic build: per-wave cycle split of the K2b scan (stats boruvka_prof_*)
