@@ -1370,161 +1370,16 @@ __global__ __launch_bounds__(256) void knn_mfma_final16_kernel(const double *__r
     }
 }
 
-// The re-check as a 16-lane systolic sum (HDB_K1F_SYS).  The reference's sum over d
-// dimensions is one dependent chain, so a lane per candidate (knn_mfma_final16_kernel) streams a
-// whole 1 KB row by itself: 64 cache lines per wave load instruction, and rows read at the
-// latency of one lane.  Here lane j of a query's 16-lane group owns dimensions [j DPL, (j+1) DPL)
-// of the query (registers) and, at step t, adds its squared differences -- in dimension order --
-// to the partial sum lane j-1 produced at step t-1 (DPP row shift) for survivor c = t - j: the
-// same additions in the same order as the sequential loop, bit for bit.  Lane 15's output is a
-// finished sum.  A step reads 16 half-lines (one 64-byte segment per lane) instead of 64 lines,
-// segments are prefetched PF steps ahead, and the survivors' rows are resolved (perm) when the
-// log is compacted.  Finished sums go to LDS; each lane keeps a top-KC of every 16th of them, and
-// the 16-lane selection of knn_mfma_final16_kernel picks the KC smallest.
-#ifndef HDB_K1F_SYS
-#define HDB_K1F_SYS 1
-#endif
-#ifndef HDB_K1F_PF
-#define HDB_K1F_PF 3  // segment prefetch distance (steps)
-#endif
-__device__ __forceinline__ double dpp_row_shr1(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), 0x111, 0xf, 0xf, false);  // row_shr:1
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x111, 0xf, 0xf, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-template <int KC, int DPL, int PF>
-__global__ __launch_bounds__(256) void knn_mfma_sys_kernel(const double *__restrict__ X, int64_t n, int d,
-                                                           const LogEnt *__restrict__ logs,
-                                                           const int *__restrict__ log_cnt,
-                                                           const float *__restrict__ thr,
-                                                           const int *__restrict__ perm,
-                                                           double *__restrict__ lists) {
-    constexpr bool REG = HDB_K1S_REGTOP && KC <= 15;
-    constexpr int NH = REG ? 2 : 1, LH = S_LOGCAP / NH;
-    __shared__ int cl_s[16][K1F_CH];     // survivors' rows in X
-    __shared__ double sv_s[16][K1F_CH];  // their exact squared distances
-    const int lane = threadIdx.x & 63, sub = lane >> 4, sl = lane & 15;
-    const int g = (threadIdx.x >> 6) * 4 + sub;  // query slot in the workgroup
-    const int64_t q = (int64_t)blockIdx.x * 16 + g;
-    const bool act = q < n && perm[q] >= 0;  // n: layout rows here (uniform per 16 lanes)
-    const int64_t qo = act ? perm[q] : 0;    // the query's row in X (the lists follow X's order)
-    const float t = act ? thr[q] : 0.f;
-    const int c0 = sl * DPL;  // this lane's dimensions [c0, c0 + DPL) of [0, d)
-    double qd[DPL];
-#pragma unroll
-    for (int u = 0; u < DPL; u++) qd[u] = (act && c0 + u < d) ? X[qo * d + c0 + u] : 0.0;
-    double top[KC];
-#pragma unroll
-    for (int k = 0; k < KC; k++) top[k] = INFINITY;
-    const unsigned long long below = (1ull << lane) - 1;
-    int *cl = cl_s[g];
-    double *sv = sv_s[g];
-    for (int h = 0; h < NH; h++) {
-        const int cnt = act ? log_cnt[NH * q + h] : 0;
-        const LogEnt *L = logs + q * S_LOGCAP + h * LH;
-        for (int j0 = 0; j0 < LH; j0 += K1F_CH) {
-            // compaction of entries [j0, j0 + K1F_CH) of this half-log (rows resolved here)
-            int np = 0;
-            for (int j1 = j0; j1 < j0 + K1F_CH; j1 += 64) {
-                LogEnt e[4];
-                bool ok[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int j = j1 + 16 * u + sl;
-                    ok[u] = j < cnt;
-                    if (ok[u]) e[u] = L[j];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const bool sv_ = ok[u] && e[u].lb <= t;
-                    const unsigned long long m = __ballot(sv_);
-                    const unsigned long long mg = (m >> (16 * sub)) & 0xFFFFull;
-                    if (sv_) cl[np + __popcll(m & below & (0xFFFFull << (16 * sub)))] = perm[e[u].cid];
-                    np += __popcll(mg);
-                }
-                if (!__ballot(j1 + 64 < cnt)) break;  // wave-uniform: the rest of the pass is empty
-            }
-            __builtin_amdgcn_wave_barrier();
-            // systolic pipeline: wave-uniform step count (the largest group of the wave)
-            int npw = np;
-            npw = max(npw, __shfl_xor(npw, 16));
-            npw = max(npw, __shfl_xor(npw, 32));
-            npw = __builtin_amdgcn_readfirstlane(npw);
-            if (npw > 0) {
-                const int steps = npw + 15;
-                // the segment this lane reads at step st: survivor st - sl (its own row when out
-                // of range: a valid address, the value is never used)
-                auto seg = [&](int st) -> const double * {
-                    const int c = st - sl;
-                    const int64_t row = (c >= 0 && c < np) ? (int64_t)cl[c] : qo;
-                    return X + row * d + c0;
-                };
-                double buf[PF][DPL];
-#pragma unroll
-                for (int p = 0; p < PF; p++) {
-                    const double *a = seg(p);
-#pragma unroll
-                    for (int u = 0; u < DPL; u++) buf[p][u] = (c0 + u < d) ? a[u] : 0.0;
-                }
-                double s_prev = 0.0;
-                for (int st0 = 0; st0 < steps; st0 += PF) {
-#pragma unroll
-                    for (int p = 0; p < PF; p++) {
-                        const int st = st0 + p;
-                        if (st < steps) {
-                            const double s_in = dpp_row_shr1(s_prev);  // lane sl-1's sum of survivor st - sl
-                            double s = sl == 0 ? 0.0 : s_in;
-#pragma unroll
-                            for (int u = 0; u < DPL; u++)
-                                if (c0 + u < d) s = s + sq_diff(qd[u], buf[p][u]);
-                            s_prev = s;
-                            const int c = st - 15;
-                            if (sl == 15 && c >= 0 && c < np) sv[c] = s;  // finished: every dimension added
-                            if (st + PF < steps) {
-                                const double *a = seg(st + PF);
-#pragma unroll
-                                for (int u = 0; u < DPL; u++) buf[p][u] = (c0 + u < d) ? a[u] : 0.0;
-                            }
-                        }
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                for (int c = sl; c < np; c += 16) topk_insert<KC>(top, sv[c]);
-                __builtin_amdgcn_wave_barrier();
-            }
-            if (!__ballot(j0 + K1F_CH < cnt)) break;  // wave-uniform: no group has more entries
-        }
-    }
-    // the KC smallest over the 16 lanes of the group
-    for (int k = 0; k < KC; k++) {
-        double mn = top[0];
-#pragma unroll
-        for (int o = 8; o >= 1; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
-        const unsigned long long b = (__ballot(top[0] == mn) >> (16 * sub)) & 0xFFFFull;
-        if (sl == __ffsll((long long)b) - 1) {
-#pragma unroll
-            for (int i = 0; i + 1 < KC; i++) top[i] = top[i + 1];
-            top[KC - 1] = INFINITY;
-        }
-        if (act && sl == 0) lists[qo * KC + k] = (mn < INFINITY) ? sqrt(mn) : JMAX;
-    }
-}
-
 template <int KC>
 static void launch_recheck(hipStream_t st, const double *X, int64_t n, int d, const LogEnt *logs, const int *log_cnt,
                            const float *thr, const int *perm, double *lists) {
-    const dim3 grid((unsigned)ceil_div(n, 16)), blk(256);
-    if (HDB_K1F_SYS && d <= 256) {
-        if (d <= 32) hipLaunchKernelGGL((knn_mfma_sys_kernel<KC, 2, HDB_K1F_PF>), grid, blk, 0, st, X, n, d, logs, log_cnt, thr, perm, lists);
-        else if (d <= 64) hipLaunchKernelGGL((knn_mfma_sys_kernel<KC, 4, HDB_K1F_PF>), grid, blk, 0, st, X, n, d, logs, log_cnt, thr, perm, lists);
-        else if (d <= 128) hipLaunchKernelGGL((knn_mfma_sys_kernel<KC, 8, HDB_K1F_PF>), grid, blk, 0, st, X, n, d, logs, log_cnt, thr, perm, lists);
-        else hipLaunchKernelGGL((knn_mfma_sys_kernel<KC, 16, HDB_K1F_PF>), grid, blk, 0, st, X, n, d, logs, log_cnt, thr, perm, lists);
-        return;
-    }
-    hipLaunchKernelGGL((knn_mfma_final16_kernel<KC>), grid, blk, (unsigned)(16 * 8 * d), st, X, n, d, logs, log_cnt,
-                       thr, perm, lists);
+    // (a 16-lane systolic variant -- lane j adds dimension block j to lane j-1's partial sum of
+    // the previous step, the reference's order -- was built and measured in round 4: 27.5 ms at
+    // C4 against this kernel's 15.5 ms; its staggered 64-byte segment reads touch 64 cache lines
+    // per instruction with little reuse, where a lane streaming its own row reuses each line
+    // over eight loads)
+    hipLaunchKernelGGL((knn_mfma_final16_kernel<KC>), dim3((unsigned)ceil_div(n, 16)), dim3(256),
+                       (unsigned)(16 * 8 * d), st, X, n, d, logs, log_cnt, thr, perm, lists);
 }
 
 // ---------------------------------------------------------------- host

@@ -499,6 +499,12 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
 #ifndef HDB_BOR_LEAF_PUBLISH
 #define HDB_BOR_LEAF_PUBLISH 0  // K2b: publish a better edge to the component bound at once (A/B r04: the same-address atomics cost more than the pruning they buy, scan 4.35 -> 3.90 ms; the wave tail still publishes)
 #endif
+#ifndef HDB_BOR_ROWS
+#define HDB_BOR_ROWS 1  // K2b leaf groups needed by few lanes: (query, candidate) pairs in 16-lane rows
+#endif
+#ifndef HDB_BOR_ROWS_MAX
+#define HDB_BOR_ROWS_MAX 16  // ... when at most this many lanes need the group (else the candidate loop)
+#endif
 #ifndef HDB_BOR_TWOPASS
 #define HDB_BOR_TWOPASS 0  // K2b/K1t leaf groups: distances first, exact updates on the hits only (A/B r04: slower -- K1t 2.05 -> 2.28 ms, scan +0.15 ms: the loop is VALU-issue bound, not a dependent chain)
 #endif
@@ -704,6 +710,15 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
 #if HDB_BOR_SUBTEST
     __shared__ double sg_s[4][8 * 2 * D];
 #endif
+#if HDB_BOR_ROWS
+    // row-batched leaf groups: the wave's query points (staged once) and per group the needing
+    // lanes' bounds and the passing pairs' keys
+    __shared__ double rq_x[4][BT * D];
+    __shared__ double rq_core[4][BT], rq_sb[4][BT];
+    __shared__ int32_t rq_comp[4][BT], rq_id[4][BT], rq_lane[4][BT];
+    __shared__ double rk_w[4][BT], rk_s[4][BT];
+    __shared__ int32_t rk_lo[4][BT], rk_hi[4][BT];
+#endif
     const int w = threadIdx.x >> 6;
     double *bxs = boxs_s[w];
     int32_t *bxt = boxt_s[w];
@@ -740,6 +755,13 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
 #pragma unroll
         for (int c = 0; c < D; c++) mx[c] = 0;
     }
+#if HDB_BOR_ROWS
+#pragma unroll
+    for (int c = 0; c < D; c++) rq_x[w][lane * D + c] = mx[c];
+    rq_core[w][lane] = mcore;
+    rq_comp[w][lane] = mcomp;
+    rq_id[w][lane] = mid;
+#endif
     Best b{INFINITY, INFINITY, INT32_MAX, INT32_MAX};
     if (valid && best_w[i] < INFINITY) b = Best{best_w[i], best_s[i], best_lo[i], best_hi[i]};  // seed_kernel
     double cb2 = INFINITY;  // padded square of the component bound
@@ -949,6 +971,69 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
             if (!__any(need)) continue;
             const int q0 = gi * SG;
             const int nq = (int)min<int64_t>(SG, n - (idx * BT + q0));
+#if HDB_BOR_ROWS
+            // Few lanes need the group (typically 3-5 of 64): the wave-uniform candidate loop
+            // spends 16 iterations on all 64 lanes for them.  Instead the (needing lane,
+            // candidate) pairs are laid out four queries x 16 candidates per wave instruction
+            // (one 16-lane row per query), the passing pairs' keys (w, s, lo, hi) parked in LDS,
+            // and each needing lane folds its row's passers into its best with key_less.  The
+            // filter uses the group-start bound (only looser: a candidate it rejects cannot beat
+            // the lane's best then or later), and the key order is a strict total order, so the
+            // best edge is the one the sequential loop finds.
+            const unsigned long long M = __ballot(need);
+            const int K = __popcll(M);
+            if (K <= HDB_BOR_ROWS_MAX) {
+                const int rank = __popcll(M & ((1ull << lane) - 1));
+                if (need) {
+                    rq_sb[w][lane] = sb;
+                    rq_lane[w][rank] = lane;
+                }
+                __builtin_amdgcn_wave_barrier();
+                const int row = lane >> 4, c = lane & 15;
+                const LRec<D> r = cand[q0 + c];  // the row's candidate (4-way LDS broadcast)
+                for (int r0 = 0; r0 < K; r0 += 4) {
+                    const int qr = r0 + row;
+                    const bool rowact = qr < K;
+                    const int ql = rq_lane[w][rowact ? qr : 0];
+                    double s2 = sq_diff(rq_x[w][ql * D], r.x[0]);
+#pragma unroll
+                    for (int cc = 1; cc < D; cc++) s2 = s2 + sq_diff(rq_x[w][ql * D + cc], r.x[cc]);
+                    const bool pair = rowact & (c < nq) & (r.comp != rq_comp[w][ql]);
+                    if (STATS) nev += pair ? 1 : 0;  // pair evaluated for a lane that needs it
+                    const bool pass = pair & (s2 <= rq_sb[w][ql]);  // also drops NaN
+                    if (pass) {
+                        double mrd = sqrt(s2);  // HDBSCANStar.java:162-168 order
+                        const double qc = rq_core[w][ql];
+                        if (qc > mrd) mrd = qc;
+                        if (r.core > mrd) mrd = r.core;
+                        const int32_t qid = rq_id[w][ql];
+                        rk_w[w][lane] = mrd;
+                        rk_s[w][lane] = s2;
+                        rk_lo[w][lane] = qid < r.id ? qid : r.id;
+                        rk_hi[w][lane] = qid < r.id ? r.id : qid;
+                    }
+                    const unsigned long long pm = __ballot(pass);
+                    __builtin_amdgcn_wave_barrier();
+                    if (need && rank >= r0 && rank < r0 + 4) {
+                        const int rr = rank - r0;
+                        unsigned bits = (unsigned)(pm >> (16 * rr)) & 0xFFFFu;
+                        while (bits) {
+                            const int k = 16 * rr + __builtin_ctz(bits);
+                            bits &= bits - 1;
+                            const double kw = rk_w[w][k], ks = rk_s[w][k];
+                            const int32_t klo = rk_lo[w][k], khi = rk_hi[w][k];
+                            if (key_less(kw, ks, klo, khi, b)) {
+                                b = Best{kw, ks, klo, khi};
+                                sb = own_sb();
+                                found = true;
+                            }
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+                continue;
+            }
+#endif
 #if HDB_BOR_TWOPASS
             // Pass 1: the group's squared distances against the bound at the group's start --
             // independent candidates, so their LDS reads and FP64 chains overlap (the one-pass
