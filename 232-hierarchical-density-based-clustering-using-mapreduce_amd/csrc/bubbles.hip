@@ -14,6 +14,9 @@
 // last-writer prefix of these logs -- resolved by the host epilogue in point order.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <cmath>
+
 #include "common.hpp"
 
 namespace hdb {
@@ -381,9 +384,16 @@ __global__ __launch_bounds__(256) void bubble_knn_replay_kernel(const double *__
 template <int KC>
 static void bubble_knn_launch(hdb_ctx *ctx, const double *rep, const double *eB, const double *nnB, int64_t b, int d,
                               int metric, int K, double *knn_out, int32_t *log_out) {
-    // chunks: >= ~256k threads per model, >= 256 candidates per chunk
+    // chunks: >= ~256k threads per model, >= 256 candidates per chunk, and short enough that a
+    // chunk's expected insertions in random order, K (1 + ln(L / K)) for L candidates, stay
+    // under half the BK_EV it can record (at K >= 7 a 1k-candidate chunk overflows
+    // most of the time, and the plain scan then runs after the split anyway) -- L <= K e^(32/K - 1);
+    // when that is below 256 the plain scan runs directly
     int64_t S = std::min<int64_t>(ceil_div(262144, std::max<int64_t>(b, 1)), std::max<int64_t>(b / 256, 1));
-    S = std::max<int64_t>(1, std::min<int64_t>(S, 64));
+    const double lmax = K * std::exp(0.5 * BK_EV / K - 1.0);
+    if (lmax < 256.0) S = 1;
+    else S = std::max<int64_t>(S, (int64_t)std::ceil((double)b / lmax));
+    S = std::max<int64_t>(1, std::min<int64_t>({S, (int64_t)64, std::max<int64_t>(b / 256, 1)}));
     if (!ctx->bubble_knn_split) S = 1;
     const dim3 g1((unsigned)ceil_div(b, 256));
     if (S > 1) {

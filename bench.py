@@ -513,6 +513,7 @@ def run_partitioned(args, workload):
                 "kernels_s": {k: round(v[0] / args.steps, 4) for k, v in sorted(kt.items(), key=lambda x: -x[1][0])},
                 "kernel_launches": {k: v[1] // args.steps for k, v in kt.items()},
                 "prim_coop_plain_retries": coop_retries,
+                "bubble_knn_replay_overflows": stat_total("bubble_knn_replay_overflows"),
                 "predicted_scaling": predicted_scaling(drv, importlib.import_module(PKG + ".parallel"))
                 if args.phases and world == 1 else None,
                 "roofline": partitioned_roofline(kt, coop_steps, coop_launches, args.steps)}
