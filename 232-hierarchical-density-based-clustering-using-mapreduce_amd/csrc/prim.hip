@@ -1054,7 +1054,14 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
             else if (lane < 3 + 2 * ND)
                 dst = grow + ((size_t)buf * nwg + bid) * (2 * ND) + (lane - 3);
             if (dst) {
-                if (local)  // plain store: the line stays in the XCD's L2 the other blocks poll
+                // local: a plain (workgroup-scope) store -- the line stays in the XCD's L2, which
+                // every CU of that XCD polls with agent-scope loads.  This relies on gfx950
+                // details the HIP memory model does not promise (a write-through L1 and one L2
+                // per XCD; every working block checked to be on one XCC above).  Correctness never
+                // depends on it: each granule carries its step tag, and if the values were not
+                // seen the plain attempt times out and the cooperative launch (agent-scope
+                // stores) runs instead -- visible as prim_coop_plain_retries in the C3/C5 lines
+                if (local)
                     __hip_atomic_store(dst, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 else
                     __hip_atomic_store(dst, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
