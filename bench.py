@@ -138,10 +138,10 @@ MFMA_BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
 # HBM bytes per launch from the PMC passes of this build (FETCH_SIZE / WRITE_SIZE runs of their
 # own, corrected by tools/pmc_summary.py): tools/profile_bench.sh (C2), tools/profile_c4.sh (C4)
 PMC_C2 = next((p for p in (os.path.join(ROOT, "profiles", r, "final", "prof_c2", "pmc_summary.json")
-                            for r in ("r03", "r02")) if os.path.exists(p)),
+                            for r in ("r04", "r03", "r02")) if os.path.exists(p)),
               os.path.join(ROOT, "profiles", "r02", "final", "prof_c2", "pmc_summary.json"))
 PMC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, "c4_final", "pmc_summary.json")
-                            for r in ("r03", "r02")) if os.path.exists(p)),
+                            for r in ("r04", "r03", "r02")) if os.path.exists(p)),
               os.path.join(ROOT, "profiles", "r02", "c4_final", "pmc_summary.json"))
 
 
