@@ -61,29 +61,6 @@ __device__ __forceinline__ unsigned long long mrd_key(double v) {
     return v == 0.0 ? 0ull : (unsigned long long)__double_as_longlong(v);
 }
 
-// Wave-wide min of a u64 through DPP moves (quad perms, row shifts, row broadcasts): no LDS
-// round trip per stage, unlike __shfl_xor.  The minimum lands in lane 63 and is broadcast.
-#define HDB_DPP_MIN_STEP(x, CTRL, ROWMASK)                                                                  \
-    do {                                                                                                    \
-        const unsigned lo_ = (unsigned)(x), hi_ = (unsigned)((x) >> 32);                                    \
-        const unsigned lo2_ = (unsigned)__builtin_amdgcn_update_dpp((int)lo_, (int)lo_, CTRL, ROWMASK, 0xf, false); \
-        const unsigned hi2_ = (unsigned)__builtin_amdgcn_update_dpp((int)hi_, (int)hi_, CTRL, ROWMASK, 0xf, false); \
-        const unsigned long long y_ = ((unsigned long long)hi2_ << 32) | lo2_;                              \
-        (x) = y_ < (x) ? y_ : (x);                                                                          \
-    } while (0)
-
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x) {
-    HDB_DPP_MIN_STEP(x, 0xb1, 0xf);   // quad_perm [1,0,3,2]
-    HDB_DPP_MIN_STEP(x, 0x4e, 0xf);   // quad_perm [2,3,0,1]
-    HDB_DPP_MIN_STEP(x, 0x114, 0xf);  // row_shr:4
-    HDB_DPP_MIN_STEP(x, 0x118, 0xf);  // row_shr:8
-    HDB_DPP_MIN_STEP(x, 0x142, 0xa);  // row_bcast:15
-    HDB_DPP_MIN_STEP(x, 0x143, 0xc);  // row_bcast:31
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)x, 63);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(x >> 32), 63);
-    return ((unsigned long long)hi << 32) | lo;
-}
-
 // highest lane whose predicate holds (-1: none)
 __device__ __forceinline__ int last_lane(bool p) {
     const unsigned long long m = __ballot(p);

@@ -1104,11 +1104,27 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
 #endif
         }
         prof.mark(7);
+        if (HDB_BOR_LEAF_PUBLISH == 2) {
+            // wave-aggregated publish: when every lane with a better edge shares one component
+            // (the late rounds' common case), one DPP minimum and at most one atomic per wave
+            const bool pub = found && (b.w * b.w) * (1.0 + 1e-12) < cb2;
+            const unsigned long long pm = __ballot(pub);
+            if (pm) {
+                const int first = __ffsll((long long)pm) - 1;
+                const int32_t c0 = __shfl(mcomp, first);
+                if (!__any(pub && mcomp != c0)) {
+                    const unsigned long long m = wave_min_u64(pub ? (unsigned long long)dbits(b.w) : ~0ull);
+                    if (lane == first &&
+                        m < __hip_atomic_load(&comp_w[c0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                        atomicMin(&comp_w[c0], m);
+                }
+            }
+        }
         if (found) {
             const double c2 = (b.w * b.w) * (1.0 + 1e-12);
             if (c2 < cb2) {
                 const unsigned long long bw = (unsigned long long)dbits(b.w);
-                if (HDB_BOR_LEAF_PUBLISH &&
+                if (HDB_BOR_LEAF_PUBLISH == 1 &&
                     bw < __hip_atomic_load(&comp_w[mcomp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                     atomicMin(&comp_w[mcomp], bw);
                 cb2 = c2;
