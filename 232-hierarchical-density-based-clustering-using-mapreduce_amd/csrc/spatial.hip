@@ -545,6 +545,30 @@ struct NoProf {
     __device__ __forceinline__ void mark(int) {}
 };
 
+// Cross-lane helpers without the LDS crossbar (__shfl is a ds_bpermute: ~60 cycles per use on
+// the traversal's dependent path): DPP within 8-lane subgroups, readlane broadcasts for ranking.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp((int)b, (int)b, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// max over the lane's 8-lane subgroup: quad swaps, then the other quad (row_half_mirror)
+__device__ __forceinline__ double sub8_max(double m) {
+    m = fmax(m, dpp_f64<0xb1>(m));   // quad_perm [1,0,3,2]
+    m = fmax(m, dpp_f64<0x4e>(m));   // quad_perm [2,3,0,1]
+    return fmax(m, dpp_f64<0x141>(m));  // row_half_mirror
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+#ifndef HDB_TRAV_DPP
+#define HDB_TRAV_DPP 1  // K1t/K2b traversal: DPP subgroup maxima and readlane ranking instead of __shfl
+#endif
+
 // Pushes the children of internal node (lev, idx) that some lane needs, farthest first
 // (so the nearest is popped first), ordered by box-to-box distance from the query box.
 // needs(a, b, tag): does this lane need the box [a, b] with that tag.  The per-child test
@@ -584,7 +608,7 @@ __device__ __forceinline__ void push_children(const Bvh &bvh, const int64_t *off
     int rank = 0;
 #pragma unroll
     for (int j = 0; j < FAN; j++) {
-        const double kj = __shfl(key, j);
+        const double kj = HDB_TRAV_DPP ? readlane_f64(key, j) : __shfl(key, j);
         const bool okj = (okmask >> j) & 1u;
         rank += (okj && (kj > key || (kj == key && j < lane))) ? 1 : 0;
     }
@@ -654,7 +678,7 @@ __device__ __forceinline__ void push_children_sub(const Bvh &bvh, const int64_t 
     int rank = 0;
 #pragma unroll
     for (int j = 0; j < FAN; j++) {
-        const double kj = __shfl(key, j);
+        const double kj = HDB_TRAV_DPP ? readlane_f64(key, j) : __shfl(key, j);
         const bool okj = (okmask >> j) & 1u;
         rank += (okj && (kj > key || (kj == key && j < lane))) ? 1 : 0;
     }
@@ -850,6 +874,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
     // the subgroup's largest bound over its lanes still searching (-1: none)
     auto sub_bound = [&]() -> double {
         double m = (search & !(mlb > cwv)) ? bound() : -1.0;
+        if (HDB_TRAV_DPP) return sub8_max(m);
 #pragma unroll
         for (int off = 1; off < 8; off <<= 1) m = fmax(m, __shfl_xor(m, off));
         return m;
