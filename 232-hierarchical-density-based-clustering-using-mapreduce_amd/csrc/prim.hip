@@ -1012,7 +1012,7 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
                 const unsigned long long gmin = wave_min_u64(qk);
                 const int q = min(last_lane(qk == gmin), NW - 1);  // all waves empty: any wave (index -1)
                 const unsigned *cw = (const unsigned *)s_cand[q];
-                const int gidx = __shfl(qi, q);
+                const int gidx = __builtin_amdgcn_readlane(qi, q);  // q is wave-uniform
                 // publish: lanes 0-2 the key granules, lanes 3 .. 3 + 2 ND the row granules
                 if (lane < 2) val = cw[2 * ND + lane];
                 else if (lane == 2) val = (unsigned)gidx;
@@ -1076,7 +1076,7 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
             }
             const unsigned long long amin = wave_min_u64(kk);
             const int k = last_lane(kk == amin);
-            const int win = __shfl(kidx, k);
+            const int win = __builtin_amdgcn_readlane(kidx, k);  // k is wave-uniform
             if (tmo || amin == KINF) {
                 if (lane == 0) s_cur = -1;
             } else {
