@@ -505,6 +505,12 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
 #ifndef HDB_BOR_ROWS_MAX
 #define HDB_BOR_ROWS_MAX 16  // ... when at most this many lanes need the group (else the candidate loop)
 #endif
+#ifndef HDB_K1T_ROWS
+#define HDB_K1T_ROWS 1  // K1t leaf groups needed by few lanes: (query, candidate) pairs in 16-lane rows
+#endif
+#ifndef HDB_K1T_ROWS_MAX
+#define HDB_K1T_ROWS_MAX 16
+#endif
 #ifndef HDB_BOR_TWOPASS
 #define HDB_BOR_TWOPASS 0  // K2b/K1t leaf groups: distances first, exact updates on the hits only (A/B r04: slower -- K1t 2.05 -> 2.28 ms, scan +0.15 ms: the loop is VALU-issue bound, not a dependent chain)
 #endif
@@ -1592,6 +1598,10 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
     __shared__ int32_t boxt_s[4][FAN];
     __shared__ int64_t lvl_s[4][2 * (MAXLEV + 1)];
     __shared__ double q_s[4][2 * D];
+#if HDB_K1T_ROWS
+    __shared__ double kq_x[4][BT * D], kq_thr[4][BT], kq_s[4][BT];
+    __shared__ int32_t kq_skip[4][BT], kq_lane[4][BT];
+#endif
     const int w = threadIdx.x >> 6;
     int64_t *off_s = lvl_s[w], *cnt_s = lvl_s[w] + MAXLEV + 1;
     const int64_t t = (int64_t)blockIdx.x * 4 + w;
@@ -1623,6 +1633,11 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
     }
     const int32_t skip_self = excl ? mid : -2;
     unsigned long long nev = 0, n_leaf = 0, n_node = 0;
+#if HDB_K1T_ROWS
+#pragma unroll
+    for (int c = 0; c < D; c++) kq_x[w][lane * D + c] = mx[c];
+    kq_skip[w][lane] = skip_self;
+#endif
 
     auto needs_vals = [&](const double (&a)[D], const double (&b)[D], int32_t) -> bool {
         return valid & (box_lb2v<D>(mx, a, b) < buf[K - 1]);
@@ -1680,6 +1695,52 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
             if (j1 <= j0) break;
             nev += (unsigned long long)(j1 - j0);
             const int q0 = gi * SG, q1 = q0 + (int)(j1 - j0);
+#if HDB_K1T_ROWS
+            // few lanes need this group (not the own tile): the (needing lane, candidate) pairs
+            // in 16-lane rows against the group-start K-th values (only looser: a rejected
+            // candidate fails the insertion test at its turn too), the passers inserted by their
+            // query lane in candidate order -- the same lists, ties included (see K2b's rows)
+            if (!own) {
+                const bool need = gneeds(gi);
+                const unsigned long long M = __ballot(need);
+                const int Kn = __popcll(M);
+                if (Kn <= HDB_K1T_ROWS_MAX) {
+                    const int rank = __popcll(M & ((1ull << lane) - 1));
+                    if (need) {
+                        kq_thr[w][lane] = buf[K - 1];
+                        kq_lane[w][rank] = lane;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    const int row = lane >> 4, c = lane & 15;
+                    const LRec<D> r = cand[q0 + c];
+                    for (int r0 = 0; r0 < Kn; r0 += 4) {
+                        const int qr = r0 + row;
+                        const bool rowact = qr < Kn;
+                        const int ql = kq_lane[w][rowact ? qr : 0];
+                        double s2 = sq_diff(kq_x[w][ql * D], r.x[0]);
+#pragma unroll
+                        for (int cc = 1; cc < D; cc++) s2 = s2 + sq_diff(kq_x[w][ql * D + cc], r.x[cc]);
+                        const bool pass = rowact & (q0 + c < q1) & (r.id != kq_skip[w][ql]) & (s2 < kq_thr[w][ql]);
+                        if (pass) kq_s[w][lane] = s2;
+                        const unsigned long long pm = __ballot(pass);
+                        __builtin_amdgcn_wave_barrier();
+                        if (need && rank >= r0 && rank < r0 + 4) {
+                            const int rr = rank - r0;
+                            unsigned bits = (unsigned)(pm >> (16 * rr)) & 0xFFFFu;
+                            while (bits) {  // ascending candidate order
+                                const int k = __builtin_ctz(bits);
+                                bits &= bits - 1;
+                                const double sv = kq_s[w][16 * rr + k];
+                                if (IDX) topk_insert_idx<K>(buf, bix, sv, (int)(tile * BT + q0 + k));
+                                else topk_insert<K>(buf, sv);
+                            }
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                    continue;
+                }
+            }
+#endif
 #if HDB_BOR_TWOPASS
             // Pass 1: the group's distances against the K-th value at the group's start
             // (independent candidates: their LDS reads and FP64 chains overlap; the K-th value
