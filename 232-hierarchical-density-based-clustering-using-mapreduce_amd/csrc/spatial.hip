@@ -497,7 +497,7 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
 #define HDB_BOR_REFRESH_LOG2 3  // K2b: re-read the component bound every 2^x node visits
 #endif
 #ifndef HDB_BOR_LEAF_PUBLISH
-#define HDB_BOR_LEAF_PUBLISH 0  // K2b: publish a better edge to the component bound at once (A/B r04: the same-address atomics cost more than the pruning they buy, scan 4.35 -> 3.90 ms; the wave tail still publishes)
+#define HDB_BOR_LEAF_PUBLISH 2  // K2b: publish a better edge to the component bound at once -- 1: per lane (round 3; its same-address atomics cost more than the pruning buys), 0: never (the wave tail still publishes), 2: one DPP minimum and at most one atomic per wave (A/B r04: scan 4.35 (1) -> 3.90 (0); 3.22 (0) -> 2.84 ms (2))
 #endif
 #ifndef HDB_BOR_ROWS
 #define HDB_BOR_ROWS 1  // K2b leaf groups needed by few lanes: (query, candidate) pairs in 16-lane rows
