@@ -505,9 +505,6 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
 #ifndef HDB_BOR_ROWS_MAX
 #define HDB_BOR_ROWS_MAX 16  // ... when at most this many lanes need the group (else the candidate loop)
 #endif
-#ifndef HDB_K1T_XCD
-#define HDB_K1T_XCD 0  // K1t: XCD-contiguous tile ranges (A/B)
-#endif
 #ifndef HDB_K1T_ROWS
 #define HDB_K1T_ROWS 1  // K1t leaf groups needed by few lanes: (query, candidate) pairs in 16-lane rows
 #endif
@@ -1607,15 +1604,8 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
 #endif
     const int w = threadIdx.x >> 6;
     int64_t *off_s = lvl_s[w], *cnt_s = lvl_s[w] + MAXLEV + 1;
-#if HDB_K1T_XCD
-    // XCD x takes one contiguous range of Morton tiles (blocks are dealt round-robin over the 8
-    // XCDs): a tile's neighbour tiles are then read through the same L2
-    const int64_t G = gridDim.x, bq = G >> 3, br = G & 7, bx = blockIdx.x & 7, bk = blockIdx.x >> 3;
-    const int64_t lb = bx < br ? bx * (bq + 1) + bk : br * (bq + 1) + (bx - br) * bq + bk;
-    const int64_t t = lb * 4 + w;
-#else
+    // (XCD-contiguous tile ranges were measured again in round 4: 1.56 -> 1.74 ms, not kept)
     const int64_t t = (int64_t)blockIdx.x * 4 + w;
-#endif
     if (t >= ntiles) return;
     const int lane = threadIdx.x & 63;
     int32_t *stk = stack_s[w];
