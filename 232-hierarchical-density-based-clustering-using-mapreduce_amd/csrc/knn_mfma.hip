@@ -1267,12 +1267,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     }
 }
 
+#ifndef HDB_K1F_U
+#define HDB_K1F_U 16
+#endif
 // exact FP64 re-check of each query's logged candidates with lb <= thr (one wave per query),
 // then the KC smallest over the wave: the same values, in the same order, as the FP64 scan
 // exact squared distance in the reference's order with the query row in LDS and the candidate
 // row streamed in 16-double chunks, the next chunk in flight while the current one is summed
 __device__ __forceinline__ double exact_sq_pf(const double *a_lds, const double *__restrict__ b, int d) {
-    constexpr int U = 16;
+    constexpr int U = HDB_K1F_U;  // doubles per prefetched chunk
     double nb[U];
 #pragma unroll
     for (int u = 0; u < U; u++) nb[u] = b[u < d ? u : d - 1];
