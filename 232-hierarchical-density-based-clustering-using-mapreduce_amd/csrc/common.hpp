@@ -54,7 +54,7 @@ struct hdb_ctx {
     std::vector<hdb::TimedLaunch> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, std::pair<double, int64_t>> acc;
-    hdb::Arena arenas[14];
+    hdb::Arena arenas[15];
     int64_t *pinned = nullptr;  // pinned_words(): async device -> host counters
     void *host_stage = nullptr;  // host_arena(): grow-only pinned staging
     size_t host_stage_bytes = 0;
@@ -100,7 +100,7 @@ namespace hdb {
 // scratch slot ids
 enum {
     A_STAGE_IN = 0, A_STAGE_OUT = 1, A_WORK0 = 2, A_WORK1 = 3, A_WORK2 = 4, A_WORK3 = 5, A_PAD = 6, A_SORT = 7,
-    A_FLAT0 = 8, A_FLAT1 = 9, A_FLAT_TMP = 10, A_LOG = 11, A_ORDER = 12, A_SBKEY = 13
+    A_FLAT0 = 8, A_FLAT1 = 9, A_FLAT_TMP = 10, A_LOG = 11, A_ORDER = 12, A_SBKEY = 13, A_XLAY = 14
 };
 
 void *arena(hdb_ctx *ctx, int slot, size_t bytes);

@@ -107,7 +107,8 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const double *__restric
                                                          int DP, const double *__restrict__ mu,
                                                          const double *__restrict__ prm, __bf16 *__restrict__ Xh,
                                                          __bf16 *__restrict__ Xl, double *__restrict__ nrm2,
-                                                         double *__restrict__ nrm, const int *__restrict__ perm) {
+                                                         double *__restrict__ nrm, const int *__restrict__ perm,
+                                                         double *__restrict__ Xlay = nullptr) {
     const double sc = prm[1];
     // one wave per row
     const int lane = threadIdx.x & 63;
@@ -117,7 +118,9 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const double *__restric
         for (int c = lane; c < DP; c += 64) {
             double v = 0;
             const int64_t src = perm ? (int64_t)perm[r] : (r < n ? r : -1);  // -1: padding row
-            if (src >= 0 && c < d) v = (X[src * d + c] - mu[c]) * sc;
+            const double x = (src >= 0 && c < d) ? X[src * d + c] : 0.0;
+            if (Xlay && c < d) Xlay[r * d + c] = x;  // the FP64 row in layout order (re-check)
+            if (src >= 0 && c < d) v = (x - mu[c]) * sc;
             const __bf16 h = to_bf16(v);
             const __bf16 l = to_bf16(v - (double)(float)h);
             Xh[r * DP + c] = h;
@@ -1267,8 +1270,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     }
 }
 
+#ifndef HDB_K1F_LAYOUT
+#define HDB_K1F_LAYOUT 1  // K1m re-check reads an FP64 copy of the rows in layout order (written by split_rows_kernel)
+#endif
 #ifndef HDB_K1F_U
-#define HDB_K1F_U 16
+#define HDB_K1F_U 8  // r04 C4 A/B: re-check 15.2 ms at 8, 15.6 at 16, 17.1 at 32
 #endif
 // exact FP64 re-check of each query's logged candidates with lb <= thr (one wave per query),
 // then the KC smallest over the wave: the same values, in the same order, as the FP64 scan
@@ -1308,7 +1314,8 @@ __global__ __launch_bounds__(256) void knn_mfma_final16_kernel(const double *__r
                                                                const int *__restrict__ log_cnt,
                                                                const float *__restrict__ thr,
                                                                const int *__restrict__ perm,
-                                                               double *__restrict__ lists) {
+                                                               double *__restrict__ lists,
+                                                               const double *__restrict__ Xlay) {
     constexpr bool REG = HDB_K1S_REGTOP && KC <= 15;
     constexpr int NH = REG ? 2 : 1, LH = S_LOGCAP / NH;
     extern __shared__ __attribute__((aligned(16))) double k1f_dyn[];
@@ -1319,8 +1326,12 @@ __global__ __launch_bounds__(256) void knn_mfma_final16_kernel(const double *__r
     const bool act = q < n && perm[q] >= 0;  // n: layout rows here (uniform per 16 lanes)
     double *qr = k1f_dyn + (size_t)g * d;
     const int64_t qo = act ? perm[q] : 0;  // the query's row in X (the lists follow X's order)
+    // Xlay: the rows in layout order, so a workgroup's 16 consecutive queries (one k-means
+    // cluster) and their candidates (the same cluster, mostly) share lines in L2 and pages in
+    // the TLB; X: the caller's order, rows gathered through perm
+    const double *qsrc = Xlay ? Xlay + q * d : X + qo * d;
     if (act)
-        for (int c = sl; c < d; c += 16) qr[c] = X[qo * d + c];
+        for (int c = sl; c < d; c += 16) qr[c] = qsrc[c];
     const float t = act ? thr[q] : 0.f;
     double top[KC];
 #pragma unroll
@@ -1353,7 +1364,8 @@ __global__ __launch_bounds__(256) void knn_mfma_final16_kernel(const double *__r
                 if (!__ballot(j1 + 64 < cnt)) break;  // wave-uniform: the rest of the pass is empty
             }
             __builtin_amdgcn_wave_barrier();
-            for (int j = sl; j < np; j += 16) topk_insert<KC>(top, exact_sq_pf(qr, X + (int64_t)perm[cl[j]] * d, d));
+            for (int j = sl; j < np; j += 16)
+                topk_insert<KC>(top, exact_sq_pf(qr, Xlay ? Xlay + (int64_t)cl[j] * d : X + (int64_t)perm[cl[j]] * d, d));
             __builtin_amdgcn_wave_barrier();
             if (!__ballot(j0 + K1F_CH < cnt)) break;  // wave-uniform: no group has more entries
         }
@@ -1375,14 +1387,14 @@ __global__ __launch_bounds__(256) void knn_mfma_final16_kernel(const double *__r
 
 template <int KC>
 static void launch_recheck(hipStream_t st, const double *X, int64_t n, int d, const LogEnt *logs, const int *log_cnt,
-                           const float *thr, const int *perm, double *lists) {
+                           const float *thr, const int *perm, double *lists, const double *Xlay) {
     // (a 16-lane systolic variant -- lane j adds dimension block j to lane j-1's partial sum of
     // the previous step, the reference's order -- was built and measured in round 4: 27.5 ms at
     // C4 against this kernel's 15.5 ms; its staggered 64-byte segment reads touch 64 cache lines
     // per instruction with little reuse, where a lane streaming its own row reuses each line
     // over eight loads)
     hipLaunchKernelGGL((knn_mfma_final16_kernel<KC>), dim3((unsigned)ceil_div(n, 16)), dim3(256),
-                       (unsigned)(16 * 8 * d), st, X, n, d, logs, log_cnt, thr, perm, lists);
+                       (unsigned)(16 * 8 * d), st, X, n, d, logs, log_cnt, thr, perm, lists, Xlay);
 }
 
 // ---------------------------------------------------------------- host
@@ -1390,7 +1402,7 @@ template <int DP, int KC>
 static void launch_single(hdb_ctx *ctx, const double *X, int64_t n, int64_t n_pad, int d, const __bf16 *Xh,
                           const __bf16 *Xl, const double *nrm2, const double *nrm, const float *cst, int excl,
                           LogEnt *logs, int *log_cnt, float *thr, int *overflow, const int *perm, const SbArgs &sb,
-                          double *lists) {
+                          double *lists, const double *Xlay) {
     hipStream_t st = ctx->stream;
     using C = ScreenCfg<DP>;
     {
@@ -1401,7 +1413,7 @@ static void launch_single(hdb_ctx *ctx, const double *X, int64_t n, int64_t n_pa
     }
     {
         KernelTimer t(ctx, "knn_mfma_final");
-        launch_recheck<KC>(st, X, n, d, logs, log_cnt, thr, perm, lists);
+        launch_recheck<KC>(st, X, n, d, logs, log_cnt, thr, perm, lists, Xlay);
         HIP_CHECK(hipGetLastError());
     }
 }
@@ -1598,10 +1610,12 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
         const int nsb = (int)sb_blk.size();
         HIP_CHECK(hipMemcpyAsync(sb_blk_d, sb_blk.data(), 4 * (size_t)nsb, hipMemcpyHostToDevice, st));
         HIP_CHECK(hipMemcpyAsync(sb_nblk_d, sb_nblk.data(), 4 * (size_t)nsb, hipMemcpyHostToDevice, st));
+        double *Xlay = nullptr;
         if (prune) {
+            if (HDB_K1F_LAYOUT) Xlay = (double *)arena(ctx, A_XLAY, 8 * (size_t)n_lp * d);
             const int g = (int)std::min<int64_t>(ceil_div(n_lp * 64, 256), 8192);
             hipLaunchKernelGGL(split_rows_kernel, dim3(g), dim3(256), 0, st, X, n, n_lp, d, DP, mu, prm, Xh, Xl, nrm2,
-                               nrm, perm);
+                               nrm, perm, Xlay);
             hipLaunchKernelGGL(ball_kernel, dim3((unsigned)(n_lp / Cf::SQ)), dim3(256), 0, st, X, d, mu, prm, perm,
                                (const int *)nullptr, (const int *)nullptr, (int64_t)Cf::SQ, DP, qctr, qrn);
             hipLaunchKernelGGL(ball_kernel, dim3((unsigned)nsb), dim3(256), 0, st, X, d, mu, prm, perm, sb_blk_d,
@@ -1650,7 +1664,7 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
 #define K1S_CASE(KK)                                                                                              \
     case KK:                                                                                                      \
         launch_single<DP, KK>(ctx, X, n_lp, n_lp, d, Xh, Xl, nrm2, nrm, cst, fl, logs, log_cnt, thr_f, overflow, \
-                              perm, sbargs, lists);                                                               \
+                              perm, sbargs, lists, Xlay);                                                         \
         break;
         switch (KC) {
             K1S_CASE(1)

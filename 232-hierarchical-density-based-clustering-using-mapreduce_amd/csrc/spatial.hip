@@ -505,6 +505,9 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
 #ifndef HDB_BOR_ROWS_MAX
 #define HDB_BOR_ROWS_MAX 16  // ... when at most this many lanes need the group (else the candidate loop)
 #endif
+// (round 4 also batched all needed groups of a leaf into one set of row passes, filtered at the
+// leaf's start, each lane recomputing its passers' distances: scan 2.84 -> 2.94 ms, 2 VGPRs
+// spilled at the 128-VGPR cap; removed)
 #ifndef HDB_K1T_ROWS
 #define HDB_K1T_ROWS 1  // K1t leaf groups needed by few lanes: (query, candidate) pairs in 16-lane rows
 #endif

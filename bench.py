@@ -543,8 +543,8 @@ def run_partitioned(args, workload):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="default 10 (c2), 5 (c4), 1 (c3/c5)")
-    ap.add_argument("--warmup", type=int, default=None, help="default 3 (c2), 2 (c4), 0 (c3/c5)")
+    ap.add_argument("--steps", type=int, default=None, help="default 30 (c2), 5 (c4), 1 (c3/c5)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 5 (c2), 2 (c4), 0 (c3/c5)")
     ap.add_argument("--n", type=int, default=N_POINTS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
@@ -553,15 +553,15 @@ def main():
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process group for N>1 (gloo: rehearse several ranks on one device)")
     ap.add_argument("--phases", action="store_true", help="c3/c5: per-phase times (synchronising)")
-    ap.add_argument("--mst-workers", type=int, default=int(os.environ.get("HDB_BENCH_MST_WORKERS", "3")),
+    ap.add_argument("--mst-workers", type=int, default=int(os.environ.get("HDB_BENCH_MST_WORKERS", "5")),
                     help="c2: partitions in flight in stage 1 (one thread, context and stream each)")
     ap.add_argument("--label-workers", type=int, default=int(os.environ.get("HDB_BENCH_LABEL_WORKERS", "2")),
                     help="c2: label stages (0: as many as --mst-workers)")
     args = ap.parse_args()
     if args.steps is None:
-        args.steps = {"c2": 10, "c4": 5}.get(args.workload, 1)
+        args.steps = {"c2": 30, "c4": 5}.get(args.workload, 1)
     if args.warmup is None:
-        args.warmup = {"c2": 3, "c4": 2}.get(args.workload, 0)
+        args.warmup = {"c2": 5, "c4": 2}.get(args.workload, 0)
     if args.workload == "c4":
         return run_c4(args)
     if args.workload != "c2":
