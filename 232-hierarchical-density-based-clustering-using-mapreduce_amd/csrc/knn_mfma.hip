@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const double *__restric
             double v = 0;
             const int64_t src = perm ? (int64_t)perm[r] : (r < n ? r : -1);  // -1: padding row
             const double x = (src >= 0 && c < d) ? X[src * d + c] : 0.0;
-            if (Xlay && c < d) Xlay[r * d + c] = x;  // the FP64 row in layout order (re-check)
+            if (Xlay) Xlay[r * DP + c] = x;  // the FP64 row in layout order, zero padded to DP (re-check)
             if (src >= 0 && c < d) v = (x - mu[c]) * sc;
             const __bf16 h = to_bf16(v);
             const __bf16 l = to_bf16(v - (double)(float)h);
@@ -1273,8 +1273,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
 #ifndef HDB_K1F_LAYOUT
 #define HDB_K1F_LAYOUT 1  // K1m re-check reads an FP64 copy of the rows in layout order (written by split_rows_kernel)
 #endif
+#ifndef HDB_K1F_WPE
+#define HDB_K1F_WPE 1  // K1m re-check: waves per SIMD the kernel is compiled for (1: no cap)
+#endif
+#ifndef HDB_K1F_DIST
+#define HDB_K1F_DIST 1  // K1m re-check: the group's running top-KC distributed over its 16 lanes
+#endif
+#ifndef HDB_K1F_LAY_UNROLL
+#define HDB_K1F_LAY_UNROLL 1
+#endif
 #ifndef HDB_K1F_U
-#define HDB_K1F_U 8  // r04 C4 A/B: re-check 15.2 ms at 8, 15.6 at 16, 17.1 at 32
+#define HDB_K1F_U 16  // doubles per prefetched chunk (r04 C4 A/B, layout rows: 8.87 ms at 8, 8.15 at 16; caller-order rows: 15.2 at 8, 15.6 at 16, 17.1 at 32)
 #endif
 // exact FP64 re-check of each query's logged candidates with lb <= thr (one wave per query),
 // then the KC smallest over the wave: the same values, in the same order, as the FP64 scan
@@ -1301,6 +1310,31 @@ __device__ __forceinline__ double exact_sq_pf(const double *a_lds, const double 
     return sx;
 }
 
+// the same sum over a layout row zero padded to DP (compile time: no guards, no clamped
+// addresses): the padded terms are (0 - 0)^2 = +0, and s + 0 == s, so the value is bit-equal
+template <int DP>
+__device__ __forceinline__ double exact_sq_lay(const double *a_lds, const double *__restrict__ b) {
+    constexpr int U = HDB_K1F_U;
+    static_assert(DP % U == 0, "chunk must divide the padded row");
+    double nb[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) nb[u] = b[u];
+    double sx = 0.0;
+#pragma unroll HDB_K1F_LAY_UNROLL
+    for (int j0 = 0; j0 < DP; j0 += U) {
+        double cb[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) cb[u] = nb[u];
+        if (j0 + U < DP) {
+#pragma unroll
+            for (int u = 0; u < U; u++) nb[u] = b[j0 + U + u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) sx = sx + sq_diff(a_lds[j0 + u], cb[u]);
+    }
+    return sx;
+}
+
 // The exact FP64 re-check, 16 lanes per query, four queries per wave: a query keeps ~KC
 // survivors, so a wave per query (round 3's kernel, 17.4 ms at C4; this one 15.6 ms) left most lanes idle while its few lanes streamed 1 KB rows
 // at HBM latency.  Per 16-lane group: the surviving log entries (lb <= thr) are compacted into
@@ -1308,8 +1342,8 @@ __device__ __forceinline__ double exact_sq_pf(const double *a_lds, const double 
 // reference's order (one lane per candidate: the sequential sum is the bit-exact one), and the
 // KC smallest come out of a 16-lane min/ballot selection.  Query rows in dynamic LDS (16 x d).
 constexpr int K1F_CH = 256;  // compacted survivors per group and pass
-template <int KC>
-__global__ __launch_bounds__(256) void knn_mfma_final16_kernel(const double *__restrict__ X, int64_t n, int d,
+template <int KC, int DP, bool LAY>
+__global__ __launch_bounds__(256, HDB_K1F_WPE) void knn_mfma_final16_kernel(const double *__restrict__ X, int64_t n, int d,
                                                                const LogEnt *__restrict__ logs,
                                                                const int *__restrict__ log_cnt,
                                                                const float *__restrict__ thr,
@@ -1324,15 +1358,21 @@ __global__ __launch_bounds__(256) void knn_mfma_final16_kernel(const double *__r
     const int g = (threadIdx.x >> 6) * 4 + sub;  // query slot in the workgroup
     const int64_t q = (int64_t)blockIdx.x * 16 + g;
     const bool act = q < n && perm[q] >= 0;  // n: layout rows here (uniform per 16 lanes)
-    double *qr = k1f_dyn + (size_t)g * d;
+    const int rs = LAY ? DP : d;  // query row length in LDS
+    double *qr = k1f_dyn + (size_t)g * rs;
     const int64_t qo = act ? perm[q] : 0;  // the query's row in X (the lists follow X's order)
     // Xlay: the rows in layout order, so a workgroup's 16 consecutive queries (one k-means
     // cluster) and their candidates (the same cluster, mostly) share lines in L2 and pages in
     // the TLB; X: the caller's order, rows gathered through perm
-    const double *qsrc = Xlay ? Xlay + q * d : X + qo * d;
+    const double *qsrc = LAY ? Xlay + q * DP : X + qo * d;
     if (act)
-        for (int c = sl; c < d; c += 16) qr[c] = qsrc[c];
+        for (int c = sl; c < rs; c += 16) qr[c] = qsrc[c];
     const float t = act ? thr[q] : 0.f;
+    // DIST: the group's running KC smallest live one per lane (lane sl: the sl-th), merged with
+    // each batch of <= 64 exact values by KC rounds of a 16-lane minimum; otherwise every lane
+    // keeps its own sorted top-KC (30 VGPRs at KC = 15) and the lanes are merged at the end
+    constexpr bool DIST = HDB_K1F_DIST && KC <= 16;
+    double lv = INFINITY;
     double top[KC];
 #pragma unroll
     for (int k = 0; k < KC; k++) top[k] = INFINITY;
@@ -1364,11 +1404,50 @@ __global__ __launch_bounds__(256) void knn_mfma_final16_kernel(const double *__r
                 if (!__ballot(j1 + 64 < cnt)) break;  // wave-uniform: the rest of the pass is empty
             }
             __builtin_amdgcn_wave_barrier();
-            for (int j = sl; j < np; j += 16)
-                topk_insert<KC>(top, exact_sq_pf(qr, Xlay ? Xlay + (int64_t)cl[j] * d : X + (int64_t)perm[cl[j]] * d, d));
+            if constexpr (DIST) {
+                int npm = max(np, __shfl_xor(np, 16));
+                npm = max(npm, __shfl_xor(npm, 32));  // wave-uniform batch count
+                for (int jb = 0; jb < npm; jb += 64) {
+                    double v[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int j = jb + 16 * i + sl;
+                        v[i] = INFINITY;
+                        if (j < np)
+                            v[i] = LAY ? exact_sq_lay<DP>(qr, Xlay + (int64_t)cl[j] * DP)
+                                        : exact_sq_pf(qr, X + (int64_t)perm[cl[j]] * d, d);
+                    }
+                    double nl = INFINITY;
+#pragma unroll 1
+                    for (int k = 0; k < KC; k++) {
+                        const double m = fmin(fmin(lv, fmin(v[0], v[1])), fmin(v[2], v[3]));
+                        double mn = m;
+#pragma unroll
+                        for (int o = 8; o >= 1; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
+                        const unsigned long long b = (__ballot(m == mn) >> (16 * sub)) & 0xFFFFull;
+                        if (sl == __ffsll((long long)b) - 1) {  // the first lane holding it gives it up
+                            if (lv == mn) lv = INFINITY;
+                            else if (v[0] == mn) v[0] = INFINITY;
+                            else if (v[1] == mn) v[1] = INFINITY;
+                            else if (v[2] == mn) v[2] = INFINITY;
+                            else v[3] = INFINITY;
+                        }
+                        if (sl == k) nl = mn;
+                    }
+                    lv = nl;
+                }
+            } else if constexpr (LAY) {
+                for (int j = sl; j < np; j += 16) topk_insert<KC>(top, exact_sq_lay<DP>(qr, Xlay + (int64_t)cl[j] * DP));
+            } else {
+                for (int j = sl; j < np; j += 16) topk_insert<KC>(top, exact_sq_pf(qr, X + (int64_t)perm[cl[j]] * d, d));
+            }
             __builtin_amdgcn_wave_barrier();
             if (!__ballot(j0 + K1F_CH < cnt)) break;  // wave-uniform: no group has more entries
         }
+    }
+    if constexpr (DIST) {
+        if (act && sl < KC) lists[qo * KC + sl] = (lv < INFINITY) ? sqrt(lv) : JMAX;
+        return;
     }
     // the KC smallest over the 16 lanes of the group
     for (int k = 0; k < KC; k++) {
@@ -1385,7 +1464,7 @@ __global__ __launch_bounds__(256) void knn_mfma_final16_kernel(const double *__r
     }
 }
 
-template <int KC>
+template <int KC, int DP>
 static void launch_recheck(hipStream_t st, const double *X, int64_t n, int d, const LogEnt *logs, const int *log_cnt,
                            const float *thr, const int *perm, double *lists, const double *Xlay) {
     // (a 16-lane systolic variant -- lane j adds dimension block j to lane j-1's partial sum of
@@ -1393,8 +1472,12 @@ static void launch_recheck(hipStream_t st, const double *X, int64_t n, int d, co
     // C4 against this kernel's 15.5 ms; its staggered 64-byte segment reads touch 64 cache lines
     // per instruction with little reuse, where a lane streaming its own row reuses each line
     // over eight loads)
-    hipLaunchKernelGGL((knn_mfma_final16_kernel<KC>), dim3((unsigned)ceil_div(n, 16)), dim3(256),
-                       (unsigned)(16 * 8 * d), st, X, n, d, logs, log_cnt, thr, perm, lists, Xlay);
+    if (Xlay)
+        hipLaunchKernelGGL((knn_mfma_final16_kernel<KC, DP, true>), dim3((unsigned)ceil_div(n, 16)), dim3(256),
+                           (unsigned)(16 * 8 * DP), st, X, n, d, logs, log_cnt, thr, perm, lists, Xlay);
+    else
+        hipLaunchKernelGGL((knn_mfma_final16_kernel<KC, DP, false>), dim3((unsigned)ceil_div(n, 16)), dim3(256),
+                           (unsigned)(16 * 8 * d), st, X, n, d, logs, log_cnt, thr, perm, lists, Xlay);
 }
 
 // ---------------------------------------------------------------- host
@@ -1413,7 +1496,7 @@ static void launch_single(hdb_ctx *ctx, const double *X, int64_t n, int64_t n_pa
     }
     {
         KernelTimer t(ctx, "knn_mfma_final");
-        launch_recheck<KC>(st, X, n, d, logs, log_cnt, thr, perm, lists, Xlay);
+        launch_recheck<KC, DP>(st, X, n, d, logs, log_cnt, thr, perm, lists, Xlay);
         HIP_CHECK(hipGetLastError());
     }
 }
@@ -1612,7 +1695,7 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
         HIP_CHECK(hipMemcpyAsync(sb_nblk_d, sb_nblk.data(), 4 * (size_t)nsb, hipMemcpyHostToDevice, st));
         double *Xlay = nullptr;
         if (prune) {
-            if (HDB_K1F_LAYOUT) Xlay = (double *)arena(ctx, A_XLAY, 8 * (size_t)n_lp * d);
+            if (HDB_K1F_LAYOUT) Xlay = (double *)arena(ctx, A_XLAY, 8 * (size_t)n_lp * DP);
             const int g = (int)std::min<int64_t>(ceil_div(n_lp * 64, 256), 8192);
             hipLaunchKernelGGL(split_rows_kernel, dim3(g), dim3(256), 0, st, X, n, n_lp, d, DP, mu, prm, Xh, Xl, nrm2,
                                nrm, perm, Xlay);

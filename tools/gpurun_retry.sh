@@ -7,7 +7,7 @@ LOG=$1; TO=$2; shift 2
 for i in 1 2 3 4 5 6 7 8; do
   /usr/local/graft/bin/gpurun --timeout "$TO" -- "$@" > "$LOG" 2>&1
   rc=$?
-  if grep -q "status=transient" "$LOG" && grep -q "charged=0.0s" "$LOG"; then sleep 150; continue; fi
+  if grep -q "status=transient" "$LOG" && grep -Eq "charged=(0.0s|Nones)" "$LOG"; then sleep 150; continue; fi
   exit $rc
 done
 exit 3
