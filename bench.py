@@ -13,7 +13,7 @@ each rank labels its partition, and the merge all-gathers every rank's edge list
 before the sort (rank 0 copies the merged list out).
 
 Several partitions are in flight on one GPU (MR-HDBSCAN* maps over independent partitions):
---mst-workers stage-1 threads (exact MST + sort, own context and stream each; default 3) and
+--mst-workers stage-1 threads (exact MST + sort, own context and stream each; default 5) and
 --label-workers label stages (default 2), so one partition's latency-bound Boruvka rounds and
 flat-label kernels overlap the next partitions' work.  Every step still does all of its work.
 
