@@ -244,6 +244,9 @@ static void stable_sort_by_key(hdb_ctx *ctx, const int32_t *keys, int64_t n, int
 // best sqrt value r, ties included), and candidates are kept by (sqrt value, sample index)
 // lexicographically -- the reference's first minimum in sample order (FirstStep.java:74-85),
 // whatever order the groups are scanned in.
+#ifndef HDB_NNG_SB
+#define HDB_NNG_SB 16  // K3g: consecutive sample groups tested behind one union box first (0: off; r04 C5 A/B nearest-sample phase: 2.69-2.73 s off, 2.18 at 4, 2.09-2.33 at 8, 2.07-2.09 at 16)
+#endif
 struct NNg {
     double r, g2;  // best sqrt value, pruning guard r^2 (1 + 2^-48)
     int i;
@@ -305,7 +308,8 @@ __global__ __launch_bounds__(256) void nng_search_kernel(const double *__restric
                                                          const int32_t *__restrict__ kslot,
                                                          const int32_t *__restrict__ glo,
                                                          const int32_t *__restrict__ ghi,
-                                                         int32_t *__restrict__ out_i, double *__restrict__ out_d) {
+                                                         int32_t *__restrict__ out_i, double *__restrict__ out_d,
+                                                         const double *__restrict__ sboxes, int sb) {
     extern __shared__ double box_s[];  // ng x 2D (lo then hi), when it fits
     const bool lds_boxes = ng * 2 * D * 8 <= 65536;
     if (lds_boxes)
@@ -335,9 +339,9 @@ __global__ __launch_bounds__(256) void nng_search_kernel(const double *__restric
         for (int c = 1; c < D; c++) acc = acc + sq_diff(x[c], sr[c]);
         nng_consider(b, acc, sidx[(int64_t)hg * G + k]);
     }
-    // every group whose box can still reach the lane's best (wave-uniform loop)
-    for (int g = w_lo; g < w_hi; g++) {
-        const double *lo = bx + (int64_t)g * 2 * D, *hi = lo + D;
+    // box lower bound in the reference's summation order on monotonically rounded gaps
+    auto box_lb = [&](const double *lo) -> double {
+        const double *hi = lo + D;
         double gap0 = fmax(fmax(lo[0] - x[0], x[0] - hi[0]), 0.0);
         double lb = gap0 * gap0;
 #pragma unroll
@@ -345,8 +349,11 @@ __global__ __launch_bounds__(256) void nng_search_kernel(const double *__restric
             const double gc = fmax(fmax(lo[c] - x[c], x[c] - hi[c]), 0.0);
             lb = lb + gc * gc;
         }
-        const bool need = live && g >= g_lo && g < g_hi && g != hg && lb <= b.g2;
-        if (!__ballot(need)) continue;
+        return lb;
+    };
+    auto scan_group = [&](int g) {
+        const bool need = live && g >= g_lo && g < g_hi && g != hg && box_lb(bx + (int64_t)g * 2 * D) <= b.g2;
+        if (!__ballot(need)) return;
         for (int k = 0; k < G; k++) {
             const double *sr = Sg + ((int64_t)g * G + k) * D;  // uniform
             double acc = sq_diff(x[0], sr[0]);
@@ -354,6 +361,20 @@ __global__ __launch_bounds__(256) void nng_search_kernel(const double *__restric
             for (int c = 1; c < D; c++) acc = acc + sq_diff(x[c], sr[c]);
             if (need) nng_consider(b, acc, sidx[(int64_t)g * G + k]);
         }
+    };
+    // every group whose box can still reach the lane's best (wave-uniform loop).  sb > 0: runs of
+    // sb consecutive groups (neighbours in the split tree) behind the union of their boxes, whose
+    // bound is <= each member's (a larger box, the same monotone operations), so a run no lane
+    // can reach holds no group any lane would scan
+    if (sb > 0) {
+        for (int s0 = (w_lo / sb) * sb; s0 < w_hi; s0 += sb) {
+            const bool need_s = live && s0 + sb > g_lo && s0 < g_hi && box_lb(sboxes + (int64_t)(s0 / sb) * 2 * D) <= b.g2;
+            if (!__ballot(need_s)) continue;
+            const int e = min(s0 + sb, w_hi);
+            for (int g = max(s0, w_lo); g < e; g++) scan_group(g);
+        }
+    } else {
+        for (int g = w_lo; g < w_hi; g++) scan_group(g);
     }
     if (pos < n) {
         out_i[p] = b.i < 0 ? 0 : b.i;  // no candidate below MAX: Java's initial nearest = 0
@@ -465,6 +486,21 @@ static bool nearest_grouped(hdb_ctx *ctx, const double *X, int64_t n, const doub
     size_t tb = 0;
     HIP_CHECK(sort_pairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr, (const int32_t *)nullptr,
                          (int32_t *)nullptr, n, 0, 32, st));
+    // runs of SB groups behind one union box (HDB_NNG_SB; 0: group boxes only)
+    const int SB = HDB_NNG_SB;
+    const int ns = SB > 0 ? (ng + SB - 1) / SB : 0;
+    std::vector<double> hsb((size_t)std::max(ns, 1) * 2 * d);
+    for (int s2 = 0; s2 < ns; s2++)
+        for (int c = 0; c < d; c++) {
+            double lo = INFINITY, hi = -INFINITY;
+            for (int g = s2 * SB; g < std::min(ng, (s2 + 1) * SB); g++) {
+                lo = std::min(lo, hb[(size_t)g * 2 * d + c]);
+                hi = std::max(hi, hb[(size_t)g * 2 * d + d + c]);
+            }
+            hsb[(size_t)s2 * 2 * d + c] = lo;
+            hsb[(size_t)s2 * 2 * d + d + c] = hi;
+        }
+    const size_t o_sb = carve(8 * hsb.size());
     const size_t o_g = carve(sizeof(double) * hg.size()), o_i = carve(4 * hi_.size()), o_b = carve(8 * hb.size()),
                  o_t = carve(sizeof(KdNode) * tree.size()), o_kt = carve(16 * (size_t)nk), o_k1 = carve(4 * (size_t)n),
                  o_k2 = carve(4 * (size_t)n), o_v1 = carve(4 * (size_t)n), o_v2 = carve(4 * (size_t)n),
@@ -484,6 +520,8 @@ static bool nearest_grouped(hdb_ctx *ctx, const double *X, int64_t n, const doub
     HIP_CHECK(hipMemcpyAsync(dg, hg.data(), sizeof(double) * hg.size(), hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(di, hi_.data(), 4 * hi_.size(), hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(db, hb.data(), 8 * hb.size(), hipMemcpyHostToDevice, st));
+    double *dsb = (double *)(base + o_sb);
+    HIP_CHECK(hipMemcpyAsync(dsb, hsb.data(), 8 * hsb.size(), hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(dt, tree.data(), sizeof(KdNode) * tree.size(), hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(dkeys, ktab.data(), 4 * ktab.size(), hipMemcpyHostToDevice, st));
     KernelTimer t(ctx, "nearest_grouped");
@@ -496,7 +534,7 @@ static bool nearest_grouped(hdb_ctx *ctx, const double *X, int64_t n, const doub
 #define NNG_CASE(DD, GG)                                                                                         \
     case DD:                                                                                                     \
         hipLaunchKernelGGL((nng_search_kernel<DD, GG>), dim3(blocks), dim3(256), lds_arg, st, X, n, v2, k2, dg, \
-                           di, db, ng, kslot, dglo, dghi, out_i, out_d);                                         \
+                           di, db, ng, kslot, dglo, dghi, out_i, out_d, dsb, SB);                                \
         break;
     switch (d) {
         NNG_CASE(2, 32)

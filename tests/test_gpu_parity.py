@@ -671,3 +671,21 @@ def test_nearest_grouped_keyed(pkg, oracle):
     idx, dist = pkg.nearest_sample(X, S, None, xk, sk, with_dist=True)
     r_idx, r_dist = oracle.nearest_sample(X, S, x_key=xk, s_key=sk)
     assert eq(idx, r_idx) and eq(dist, r_dist)
+
+
+@pytest.mark.parametrize("d", [3, 8])
+def test_nearest_grouped_keyed_vs_oracle(pkg, oracle, d):
+    """Keyed K3g (the per-subset levels of C3/C5): uneven key sizes, so the runs of consecutive
+    sample groups tested behind one union box (HDB_NNG_SB) straddle key boundaries, and a key
+    without samples (index 0 / MAX, the Java init)."""
+    rng = np.random.default_rng(50 + d)
+    n = 24000
+    X = np.round(blobs(n, d, 9, 60 + d), 1)
+    xk = rng.choice(9, n, p=[0.3, 0.2, 0.15, 0.1, 0.08, 0.07, 0.05, 0.04, 0.01]).astype(np.int32)
+    S = X[::11].copy()
+    sk = xk[::11].copy()
+    sk[sk == 8] = 7  # key 8 has no samples
+    assert S.shape[0] >= 1024
+    idx, dist = pkg.nearest_sample(X, S, None, xk, sk, with_dist=True)
+    r_idx, r_dist = oracle.nearest_sample(X, S, x_key=xk, s_key=sk)
+    assert eq(idx, r_idx) and eq(dist, r_dist)
