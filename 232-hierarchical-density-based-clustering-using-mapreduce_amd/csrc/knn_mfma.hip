@@ -1285,10 +1285,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
 #ifndef HDB_K1F_U
 #define HDB_K1F_U 16  // doubles per prefetched chunk (r04 C4 A/B, layout rows: 8.87 ms at 8, 8.15 at 16; caller-order rows: 15.2 at 8, 15.6 at 16, 17.1 at 32)
 #endif
-// exact FP64 re-check of each query's logged candidates with lb <= thr (one wave per query),
-// then the KC smallest over the wave: the same values, in the same order, as the FP64 scan
 // exact squared distance in the reference's order with the query row in LDS and the candidate
-// row streamed in 16-double chunks, the next chunk in flight while the current one is summed
+// row (caller order, runtime length d) streamed in U-double chunks, the next chunk in flight
+// while the current one is summed
 __device__ __forceinline__ double exact_sq_pf(const double *a_lds, const double *__restrict__ b, int d) {
     constexpr int U = HDB_K1F_U;  // doubles per prefetched chunk
     double nb[U];
@@ -1336,11 +1335,14 @@ __device__ __forceinline__ double exact_sq_lay(const double *a_lds, const double
 }
 
 // The exact FP64 re-check, 16 lanes per query, four queries per wave: a query keeps ~KC
-// survivors, so a wave per query (round 3's kernel, 17.4 ms at C4; this one 15.6 ms) left most lanes idle while its few lanes streamed 1 KB rows
-// at HBM latency.  Per 16-lane group: the surviving log entries (lb <= thr) are compacted into
-// LDS 256 at a time, every lane computes the exact FP64 distances of its survivors in the
-// reference's order (one lane per candidate: the sequential sum is the bit-exact one), and the
-// KC smallest come out of a 16-lane min/ballot selection.  Query rows in dynamic LDS (16 x d).
+// survivors, so a wave per query (round 3's kernel, 17.4 ms at C4) left most lanes idle while its
+// few lanes streamed 1 KB rows.  Per 16-lane group: the surviving log entries (lb <= thr) are
+// compacted into LDS 256 at a time, every lane computes the exact FP64 distances of its
+// survivors in the reference's order (one lane per candidate: the sequential sum is the
+// bit-exact one), and the KC smallest come out of 16-lane min/ballot selections.  LAY: the rows
+// are read from the zero-padded layout copy with the compile-time length DP (16-byte loads, no
+// clamps: half the L1 accesses of the caller-order path; 15.6 -> 7.3 ms at C4 with DIST).
+// Query rows in dynamic LDS (16 x DP, or 16 x d).
 constexpr int K1F_CH = 256;  // compacted survivors per group and pass
 template <int KC, int DP, bool LAY>
 __global__ __launch_bounds__(256, HDB_K1F_WPE) void knn_mfma_final16_kernel(const double *__restrict__ X, int64_t n, int d,
