@@ -500,6 +500,7 @@ def run_partitioned(args, workload):
                 "data": f"synthetic (seeded Gaussian blobs, seed {cfg['seed']})",
                 "config": {"workload": cfg["desc"], "points": n, "d": cfg["d"], "min_pts": MIN_PTS,
                            "min_cl_size": MIN_CL_SIZE, "prim_leaf_max": drv.prim_leaf_max,
+                           "model_threads": drv.model_threads,
                            "parallelism": f"sharded driver x{world} (leaves/local models by LPT, "
                                           f"point-chunked nearest sample, RCCL merge)"},
                 "iterations": r["iterations"], "n_clusters": r["n_clusters"],
