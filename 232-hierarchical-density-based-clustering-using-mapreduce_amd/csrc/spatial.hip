@@ -503,7 +503,7 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
 #define HDB_BOR_ROWS 1  // K2b leaf groups needed by few lanes: (query, candidate) pairs in 16-lane rows
 #endif
 #ifndef HDB_BOR_ROWS_MAX
-#define HDB_BOR_ROWS_MAX 8  // ... when at most this many lanes need the group (else the candidate loop; r04 A/B scan: 2.81 ms at 8, 2.84 at 16, 2.97 at 32, 4.1 at 64)
+#define HDB_BOR_ROWS_MAX 8  // ... when at most this many lanes need the group (else the candidate loop; r04 A/B scan: 2.85 ms at 4, 2.81 at 8, 2.84 at 16, 2.97 at 32, 4.1 at 64; K1t at 8: 1.58 vs 1.56 ms at 16)
 #endif
 // (round 4 also batched all needed groups of a leaf into one set of row passes, filtered at the
 // leaf's start, each lane recomputing its passers' distances: scan 2.84 -> 2.94 ms, 2 VGPRs
