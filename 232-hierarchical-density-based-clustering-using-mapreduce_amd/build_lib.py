@@ -17,7 +17,7 @@ OUT = os.environ.get("HDBMI_OUT") or os.path.join(HERE, "lib")
 LIB = os.path.join(OUT, "libhdbmi.so")
 SOURCES = ["context.cpp", "capi.cpp", "local_model.cpp", "flat.cpp", "formats.cpp", "knn.hip", "nearest.hip", "prim.hip",
            "bubbles.hip", "merge.hip", "spatial.hip", "knn_mfma.hip", "flat.hip", "comm.cpp"] + [f"knn_d{d}.hip" for d in (1, 2, 3, 4, 5, 6, 8, 16)]
-HEADERS = ["common.hpp", "internal.hpp", "knn_impl.hpp", "sort.hpp"]
+HEADERS = ["common.hpp", "internal.hpp", "knn_impl.hpp", "sort.hpp", "ssort.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # -ffp-contract=off: the reference (Java) never fuses a*b+c; bit-exact parity needs the same.

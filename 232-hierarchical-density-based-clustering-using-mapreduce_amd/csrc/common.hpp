@@ -54,7 +54,7 @@ struct hdb_ctx {
     std::vector<hdb::TimedLaunch> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, std::pair<double, int64_t>> acc;
-    hdb::Arena arenas[15];
+    hdb::Arena arenas[16];
     int64_t *pinned = nullptr;  // pinned_words(): async device -> host counters
     void *host_stage = nullptr;  // host_arena(): grow-only pinned staging
     size_t host_stage_bytes = 0;
@@ -91,6 +91,9 @@ struct hdb_ctx {
     int flat_link_variant = 1;  // K6 dc_link A/B: 0 direct guarded atomics, 1 LDS-combined multi-batch
     int flat_root_variant = 3;  // K6 dc_root A/B: 0 LDS table (256 threads), 1 (1024), 2 direct atomics, 3-5 multi-batch
     int flat_block_log = 10;   // K6: deep depths per workgroup in LDS (2^x ranks, 8-10; 0: the sequential dc_local)
+    bool ssort = true;         // sample sort (ssort.hpp) for the Morton order, the edge orders and K6's term sort
+                               // (false: the rocPRIM radix chains; A/B and tests)
+    int ssort_cap = 0;         // ssort bucket size sorted in LDS (0: SS_CAP; tests lower it to run the merge path)
     bool count_evals = false;  // K1t counts evaluated pairs (diagnostic; costs one sync)
     std::map<std::string, int64_t> stats;  // diagnostic counters (count_evals)
 };
@@ -100,7 +103,8 @@ namespace hdb {
 // scratch slot ids
 enum {
     A_STAGE_IN = 0, A_STAGE_OUT = 1, A_WORK0 = 2, A_WORK1 = 3, A_WORK2 = 4, A_WORK3 = 5, A_PAD = 6, A_SORT = 7,
-    A_FLAT0 = 8, A_FLAT1 = 9, A_FLAT_TMP = 10, A_LOG = 11, A_ORDER = 12, A_SBKEY = 13, A_XLAY = 14
+    A_FLAT0 = 8, A_FLAT1 = 9, A_FLAT_TMP = 10, A_LOG = 11, A_ORDER = 12, A_SBKEY = 13, A_XLAY = 14,
+    A_SS = 15  // ssort.hpp scratch
 };
 
 void *arena(hdb_ctx *ctx, int slot, size_t bytes);

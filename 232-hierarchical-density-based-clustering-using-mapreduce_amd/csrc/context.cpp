@@ -172,6 +172,7 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         if (const char *e = getenv("HDB_FLAT_LINK")) c->flat_link_variant = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_FLAT_ROOT")) c->flat_root_variant = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_MERGE_RUNS")) c->merge_runs = atoi(e) != 0;      // A/B knob
+        if (const char *e = getenv("HDB_SSORT")) c->ssort = atoi(e) != 0;                // A/B knob
         *out = c;
         return HDB_OK;
     } catch (const Error &e) {
@@ -353,6 +354,15 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
     }
     if (k == "boruvka_knn_seed") {
         ctx->boruvka_knn_seed = value != 0;
+        return HDB_OK;
+    }
+    if (k == "ssort") {
+        ctx->ssort = value != 0;
+        return HDB_OK;
+    }
+    if (k == "ssort_cap") {
+        if (value < 0 || value > 4096) return HDB_EINVAL;
+        ctx->ssort_cap = (int)value;
         return HDB_OK;
     }
     if (k == "count_evals") {

@@ -35,6 +35,7 @@
 #include "common.hpp"
 #include "internal.hpp"
 #include "sort.hpp"
+#include "ssort.hpp"
 
 namespace hdb {
 
@@ -813,6 +814,22 @@ __global__ void fl_terms(const int32_t *__restrict__ top, const int32_t *__restr
     }
 }
 
+// ssort functors of the stability terms' order: (cluster, descending level) keys, ties (the
+// non-terms' all-ones keys) by position -- the stable radix order
+struct TermKeyF {
+    const uint64_t *key;
+    __device__ SKey operator()(int64_t i) const { return SKey{key[i], (uint64_t)i}; }
+};
+struct TermEmitF {
+    const double *val;
+    uint64_t *key_out;
+    double *val_out;
+    __device__ void operator()(int64_t r, const SKey &k) const {
+        key_out[r] = k.hi;
+        val_out[r] = val[k.lo];
+    }
+};
+
 // one wave per cluster: lanes stage the chain's terms through LDS (coalesced, the next chunk
 // in flight), lane 0 adds them in order -- the host's sequential sum, descending level
 constexpr int STAB_CHUNK = 256;
@@ -1567,7 +1584,10 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
                        key1, val1, err);
     int kb = 0;
     while ((int64_t(1) << kb) < m + 1) kb++;
-    {
+    const SsPlan tpl = ss_plan(m, ctx->ssort_cap);
+    if (ctx->ssort && tpl.nb) {  // the terms' keys are unique (rank in the low word); non-terms last
+        ssort(tpl, (char *)arena(ctx, A_SS, tpl.bytes), TermKeyF{key1}, TermEmitF{val1, key2, val2}, st);
+    } else {
         size_t tb = 0;
         // keys of non-terms are all-ones: sorting on the cluster bits + 32 keeps them last
         HIP_CHECK(sort_pairs(nullptr, tb, key1, key2, val1, val2, m, 0, 64, st));

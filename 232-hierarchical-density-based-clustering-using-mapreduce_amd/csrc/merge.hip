@@ -8,6 +8,7 @@
 
 #include "common.hpp"
 #include "sort.hpp"
+#include "ssort.hpp"
 
 namespace hdb {
 
@@ -132,10 +133,48 @@ __global__ void run_place_r_kernel(const int32_t *__restrict__ va, const int32_t
     }
 }
 
+// ssort functors of the stable descending sort: the weight (order-preserving map of doubles
+// to u64, -0.0 read as +0.0 like edge_keys_kernel's keys), ties by input position
+struct DescKeyF {
+    const double *w;
+    __device__ SKey operator()(int64_t i) const {
+        const double x = w[i];
+        const uint64_t b = (uint64_t)__double_as_longlong(x == 0.0 ? 0.0 : x);
+        return SKey{~((b >> 63) ? ~b : (b | 0x8000000000000000ull)), (uint64_t)i};
+    }
+};
+struct GatherEmitF {
+    const int32_t *va, *vb;
+    const double *w;
+    int32_t *oa, *ob;
+    double *ow;
+    __device__ void operator()(int64_t r, const SKey &k) const {
+        const int64_t p = (int64_t)k.lo;
+        oa[r] = va[p];
+        ob[r] = vb[p];
+        ow[r] = w[p];
+    }
+};
+
 // in-place stable descending sort of (va, vb, w)
 void sort_edges_desc_device(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne) {
     if (ne <= 1) return;
     if (ne > INT32_MAX) HDB_THROW(HDB_EINVAL, "too many edges for one sort");
+    if (ctx->ssort && !ctx->merge_runs) {
+        const SsPlan pl = ss_plan(ne, ctx->ssort_cap);
+        if (pl.nb) {
+            KernelTimer t(ctx, "merge_sort");
+            const size_t eb = ((size_t)ne * 4 + 255) & ~size_t(255);
+            char *tmp = (char *)arena(ctx, A_WORK3, 2 * eb + (size_t)ne * 8);
+            int32_t *ta = (int32_t *)tmp, *tb_ = (int32_t *)(tmp + eb);
+            double *tw = (double *)(tmp + 2 * eb);
+            ssort(pl, (char *)arena(ctx, A_SS, pl.bytes), DescKeyF{w}, GatherEmitF{va, vb, w, ta, tb_, tw}, ctx->stream);
+            HIP_CHECK(hipMemcpyAsync(va, ta, sizeof(int32_t) * ne, hipMemcpyDeviceToDevice, ctx->stream));
+            HIP_CHECK(hipMemcpyAsync(vb, tb_, sizeof(int32_t) * ne, hipMemcpyDeviceToDevice, ctx->stream));
+            HIP_CHECK(hipMemcpyAsync(w, tw, sizeof(double) * ne, hipMemcpyDeviceToDevice, ctx->stream));
+            return;
+        }
+    }
     size_t off = 0;
     auto carve = [&](size_t bytes) {
         size_t o = off;

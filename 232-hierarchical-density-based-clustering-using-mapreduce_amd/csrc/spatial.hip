@@ -36,6 +36,7 @@
 
 #include "internal.hpp"
 #include "sort.hpp"
+#include "ssort.hpp"
 
 namespace hdb {
 
@@ -158,23 +159,28 @@ __host__ __device__ inline int morton_bits(int d) {
     return b > 16 ? 16 : b;
 }
 
-__global__ void morton_kernel(const double *__restrict__ X, int64_t n, int d, const double *__restrict__ lo,
-                              const double *__restrict__ hi, uint64_t *__restrict__ keys, int32_t *__restrict__ iota) {
+__device__ __forceinline__ uint64_t morton_key(const double *__restrict__ x, int d, const double *__restrict__ lo,
+                                               const double *__restrict__ hi) {
     const int dk = d < 8 ? d : 8;
     const int bits = morton_bits(d);
+    uint64_t key = 0;
+    uint32_t q[8];
+    for (int c = 0; c < dk; c++) {
+        double span = hi[c] - lo[c];
+        double t = span > 0 ? (x[c] - lo[c]) / span : 0.0;
+        t = t < 0 ? 0 : (t > 1 ? 1 : t);
+        if (t != t) t = 0;
+        q[c] = (uint32_t)(t * (double)((1u << bits) - 1));
+    }
+    for (int b = bits - 1; b >= 0; b--)
+        for (int c = 0; c < dk; c++) key = (key << 1) | ((q[c] >> b) & 1u);
+    return key;
+}
+
+__global__ void morton_kernel(const double *__restrict__ X, int64_t n, int d, const double *__restrict__ lo,
+                              const double *__restrict__ hi, uint64_t *__restrict__ keys, int32_t *__restrict__ iota) {
     HDB_GRID_STRIDE(i, n) {
-        uint64_t key = 0;
-        uint32_t q[8];
-        for (int c = 0; c < dk; c++) {
-            double span = hi[c] - lo[c];
-            double t = span > 0 ? (X[i * d + c] - lo[c]) / span : 0.0;
-            t = t < 0 ? 0 : (t > 1 ? 1 : t);
-            if (t != t) t = 0;
-            q[c] = (uint32_t)(t * (double)((1u << bits) - 1));
-        }
-        for (int b = bits - 1; b >= 0; b--)
-            for (int c = 0; c < dk; c++) key = (key << 1) | ((q[c] >> b) & 1u);
-        keys[i] = key;
+        keys[i] = morton_key(X + i * d, d, lo, hi);
         iota[i] = (int32_t)i;
     }
 }
@@ -194,6 +200,32 @@ __global__ void build_recs_kernel(const double *__restrict__ X, const double *__
         inv[o] = (int32_t)i;
     }
 }
+
+// ssort functors of the index build (the Morton order, ties by input position) and of the
+// record build fused into the sort's last kernel (build_recs_kernel's output)
+template <int D>
+struct MortonKeyF {
+    const double *X;
+    const double *lo, *hi;
+    __device__ SKey operator()(int64_t i) const { return SKey{morton_key(X + i * D, D, lo, hi), (uint64_t)i}; }
+};
+template <int D>
+struct RecEmitF {
+    const double *X;
+    const double *core;
+    Rec<D> *recs;
+    int32_t *inv;
+    __device__ void operator()(int64_t r, const SKey &k) const {
+        const int32_t o = (int32_t)k.lo;
+        Rec<D> rec;
+        for (int c = 0; c < D; c++) rec.x[c] = X[(int64_t)o * D + c];
+        rec.core = core ? core[o] : 0.0;
+        rec.comp = (int32_t)r;
+        rec.id = o;
+        recs[r] = rec;
+        inv[o] = (int32_t)r;
+    }
+};
 
 // Tile boxes (coordinates fixed) and uniform-component tags (per round).  Each 64-point
 // tile is also cut into 4 sub-groups of SG = 16 consecutive points with their own box and
@@ -1425,6 +1457,52 @@ __global__ void edge_out_kernel(const int32_t *perm_, const int32_t *a, const in
     }
 }
 
+// ssort functors of the MST edge orders.  Keys: the weight through an order-preserving map
+// of doubles to u64 (-0.0 read as +0.0, as the radix path's keys), then the tie breaker:
+// tree edges (ea << 31 | eb) -- the (lo, hi) order the radix path sorts by first --, self
+// edges (1 << 62 | id) after every tree edge of equal weight (the merge's "tree edges first").
+__device__ __forceinline__ uint64_t dkey_asc(double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x == 0.0 ? 0.0 : x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double dkey_inv(uint64_t u) {
+    return __longlong_as_double((long long)((u >> 63) ? (u & 0x7fffffffffffffffull) : ~u));
+}
+constexpr uint64_t EK_SELF = 1ull << 62;
+struct TreeEdgeKeyF {  // desc: the reducers' merge order; asc: FirstStep's (w, lo, hi)
+    const int32_t *ea, *eb;
+    const double *ew;
+    const double *core;  // self edges (desc only), nullable
+    int64_t ne;
+    bool desc;
+    __device__ SKey operator()(int64_t i) const {
+        if (i < ne) {
+            const uint64_t k = dkey_asc(ew[i]);
+            return SKey{desc ? ~k : k, ((uint64_t)(uint32_t)ea[i] << 31) | (uint32_t)eb[i]};
+        }
+        const int64_t j = i - ne;
+        return SKey{~dkey_asc(core[j]), EK_SELF | (uint64_t)j};
+    }
+};
+struct TreeEdgeEmitF {
+    int32_t *va, *vb;
+    double *w;
+    const double *core;
+    bool desc;
+    __device__ void operator()(int64_t r, const SKey &k) const {
+        if (k.lo & EK_SELF) {
+            const int32_t j = (int32_t)(k.lo & 0x7fffffffu);
+            va[r] = j;
+            vb[r] = j;
+            w[r] = core[j];
+        } else {
+            va[r] = (int32_t)((k.lo >> 31) & 0x7fffffffu);
+            vb[r] = (int32_t)(k.lo & 0x7fffffffu);
+            w[r] = dkey_inv(desc ? ~k.hi : k.hi);
+        }
+    }
+};
+
 // ------------------------------------------------ fused leaf: kNN-seeded round 0
 template <int D>
 __global__ void set_core_kernel(Rec<D> *__restrict__ recs, int64_t n, const double *__restrict__ core) {
@@ -1915,15 +1993,19 @@ static Spatial<D> build_spatial(hdb_ctx *ctx, const double *X, int64_t n, const 
     const int nbb = (int)std::min<int64_t>(BBOX_BLOCKS, ceil_div(n, 256));
     hipLaunchKernelGGL(bbox_partial_kernel<D>, dim3(nbb), dim3(256), 0, st, X, n, bpart);
     hipLaunchKernelGGL(bbox_final_kernel<D>, dim3(D), dim3(64), 0, st, bpart, nbb, blo, bhi);
-    hipLaunchKernelGGL(morton_kernel, dim3(g), dim3(256), 0, st, X, n, D, blo, bhi, sp.keys, sp.iota);
-    {
+    const SsPlan pl = ss_plan(n, ctx->ssort_cap);
+    if (ctx->ssort && pl.nb) {  // Morton order + records in one sample sort
+        ssort(pl, (char *)arena(ctx, A_SS, pl.bytes), MortonKeyF<D>{X, blo, bhi},
+              RecEmitF<D>{X, core, sp.recs, sp.inv}, st);
+    } else {
+        hipLaunchKernelGGL(morton_kernel, dim3(g), dim3(256), 0, st, X, n, D, blo, bhi, sp.keys, sp.iota);
         size_t tb = 0;
         const int kbits = (D < 8 ? D : 8) * morton_bits(D);
         HIP_CHECK(sort_pairs(nullptr, tb, sp.keys, sp.keys2, sp.iota, sp.perm, n, 0, kbits, st));
         void *tmp = arena(ctx, A_SORT, tb);
         HIP_CHECK(sort_pairs(tmp, tb, sp.keys, sp.keys2, sp.iota, sp.perm, n, 0, kbits, st));
+        hipLaunchKernelGGL(build_recs_kernel<D>, dim3(g), dim3(256), 0, st, X, core, sp.perm, n, sp.recs, sp.inv);
     }
-    hipLaunchKernelGGL(build_recs_kernel<D>, dim3(g), dim3(256), 0, st, X, core, sp.perm, n, sp.recs, sp.inv);
     hipLaunchKernelGGL(tile_box_kernel<D>, dim3((unsigned)sp.ntiles), dim3(64), 0, st, sp.recs, n, sp.bvh.lo,
                        sp.bvh.hi, sp.bvh.slo, sp.bvh.shi);
     for (int L = 1; L < sp.bvh.levels; L++)
@@ -2258,7 +2340,16 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
         ctx->stats["last_evals"] = tot_evals;
     }
     // sort edges by (w, lo, hi): stable sort by (lo,hi) then stable by w
-    {
+    bool sorted = false;
+    if (ctx->ssort) {  // one sample sort: tree edges (+ self edges) straight into the outputs
+        const int64_t ne = n - 1, tot = ne + ((merged && self_core) ? n : 0);
+        const SsPlan pl = ss_plan(tot, ctx->ssort_cap);
+        if (pl.nb) {
+            sorted = ssort(pl, (char *)arena(ctx, A_SS, pl.bytes), TreeEdgeKeyF{ea, eb, ew, self_core, ne, merged},
+                           TreeEdgeEmitF{va, vb, w, self_core, merged}, st);
+        }
+    }
+    if (!sorted) {
         int64_t ne = n - 1;
         if (ne > 0) {
             uint64_t *k1 = sp.keys, *k2 = sp.keys2;
