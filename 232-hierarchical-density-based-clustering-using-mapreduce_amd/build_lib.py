@@ -8,6 +8,7 @@ import argparse
 import concurrent.futures as cf
 import hashlib
 import os
+import re
 import subprocess
 import sys
 
@@ -30,9 +31,25 @@ def _obj(src: str) -> str:
     return os.path.join(OUT, "obj", src + ".o")
 
 
+def _deps(src: str) -> list:
+    """src plus the csrc headers it includes, transitively"""
+    seen, todo = [], [src]
+    while todo:
+        f = todo.pop()
+        if f in seen:
+            continue
+        seen.append(f)
+        with open(os.path.join(CSRC, f)) as fh:
+            for line in fh:
+                m = re.match(r'\s*#\s*include\s+"([^"/]+)"', line)
+                if m and m.group(1) in HEADERS:
+                    todo.append(m.group(1))
+    return seen
+
+
 def _stamp(src: str) -> str:
     h = hashlib.sha1()
-    for f in [src, *HEADERS]:
+    for f in _deps(src):
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
     with open(os.path.join(HERE, "..", "include", "hdbmi.h"), "rb") as fh:

@@ -37,9 +37,12 @@ void *arena(hdb_ctx *ctx, int slot, size_t bytes) {
             HIP_CHECK(hipStreamSynchronize(ctx->stream));
             HIP_CHECK(hipFree(a.ptr));
             a.ptr = nullptr;
+            a.bytes = 0;
         }
         size_t nb = bytes + bytes / 4 + 4096;
-        HIP_CHECK(hipMalloc(&a.ptr, nb));
+        void *p = nullptr;
+        HIP_CHECK(hipMalloc(&p, nb));  // on failure the slot stays empty (never a stale size)
+        a.ptr = p;
         a.bytes = nb;
     }
     return a.ptr;

@@ -1697,7 +1697,16 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
         HIP_CHECK(hipMemcpyAsync(sb_nblk_d, sb_nblk.data(), 4 * (size_t)nsb, hipMemcpyHostToDevice, st));
         double *Xlay = nullptr;
         if (prune) {
-            if (HDB_K1F_LAYOUT) Xlay = (double *)arena(ctx, A_XLAY, 8 * (size_t)n_lp * DP);
+            // the layout-order FP64 copy (8 n DP bytes, ~2 GB at C4) only speeds the re-check:
+            // when the device cannot hold it, the re-check reads the caller-order rows instead
+            if (HDB_K1F_LAYOUT) {
+                try {
+                    Xlay = (double *)arena(ctx, A_XLAY, 8 * (size_t)n_lp * DP);
+                } catch (const Error &) {
+                    (void)hipGetLastError();  // clear the failed allocation's sticky error
+                    Xlay = nullptr;
+                }
+            }
             const int g = (int)std::min<int64_t>(ceil_div(n_lp * 64, 256), 8192);
             hipLaunchKernelGGL(split_rows_kernel, dim3(g), dim3(256), 0, st, X, n, n_lp, d, DP, mu, prm, Xh, Xl, nrm2,
                                nrm, perm, Xlay);

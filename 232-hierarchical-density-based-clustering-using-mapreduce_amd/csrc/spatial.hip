@@ -232,12 +232,6 @@ struct RecEmitF {
 // tag: a leaf visit skips a sub-group no lane needs (finer culling, same wave shape).
 constexpr int SG = 16;
 constexpr int NSG = BT / SG;
-#ifndef HDB_LEAF_PREFETCH
-#define HDB_LEAF_PREFETCH 0  // measured 8.74 -> 8.67 ms with per-lane tests; with HDB_BOR_SUBTEST it spills
-#endif
-#ifndef HDB_K1T_PREFETCH  // the same prefetch in K1t: off -- 82 -> 104 VGPRs drops K1t to 4
-#define HDB_K1T_PREFETCH 0  // waves/SIMD and costs more than it hides (2.0 -> 2.23 ms)
-#endif
 #ifndef HDB_K1T_WPE  // waves per EU the D <= 3 K1t is compiled for (82 VGPRs free-running: 5)
 #define HDB_K1T_WPE 5
 #endif
@@ -407,38 +401,6 @@ __device__ __forceinline__ void staged_box(const double *sb, int k, double (&a)[
     }
 }
 
-#if HDB_LEAF_PREFETCH
-// A leaf tile's records and group boxes held in registers (one element per lane), so a leaf
-// can be loaded while the wave still evaluates the previous one.  commit == stage_boxes<D,
-// NSG> + the cand[] staging.
-template <int D>
-struct LeafRegs {
-    LRec<D> r;
-    double gl = 0, gh = 0;
-    int32_t gt = -1;
-};
-template <int D>
-__device__ __forceinline__ void leaf_issue(const Rec<D> *__restrict__ recs, int64_t n, const Bvh &bvh, int64_t tile,
-                                           int lane, LeafRegs<D> &L) {
-    static_assert(NSG * D <= 64, "one group-box element per lane");
-    L.r = fetch_rec<D>(recs, n, tile * BT + lane);
-    const int e = lane < NSG * D - 1 ? lane : NSG * D - 1;  // clamped: unconditional loads
-    L.gl = bvh.slo[tile * NSG * D + e];
-    L.gh = bvh.shi[tile * NSG * D + e];
-    L.gt = bvh.stag[tile * NSG + (lane < NSG - 1 ? lane : NSG - 1)];
-}
-template <int D>
-__device__ __forceinline__ void leaf_commit(const LeafRegs<D> &L, LRec<D> *cand, double *bxs, int32_t *bxt, int lane) {
-    __builtin_amdgcn_wave_barrier();
-    if (lane < NSG * D) {
-        bxs[lane] = L.gl;
-        bxs[NSG * D + lane] = L.gh;
-    }
-    if (lane < NSG) bxt[lane] = L.gt;
-    cand[lane] = L.r;
-    __builtin_amdgcn_wave_barrier();
-}
-#endif
 
 // The BVH level table (offset and node count per level, as bvh_shape) rebuilt per wave in
 // LDS from ntiles: reading Bvh::off/cnt with a dynamic level index from the kernel arguments
@@ -545,9 +507,6 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
 #endif
 #ifndef HDB_K1T_ROWS_MAX
 #define HDB_K1T_ROWS_MAX 16
-#endif
-#ifndef HDB_BOR_TWOPASS
-#define HDB_BOR_TWOPASS 0  // K2b/K1t leaf groups: distances first, exact updates on the hits only (A/B r04: slower -- K1t 2.05 -> 2.28 ms, scan +0.15 ms: the loop is VALU-issue bound, not a dependent chain)
 #endif
 #ifndef HDB_BOR_PROF
 #define HDB_BOR_PROF 0  // diagnostic build: per-wave cycle split of the K2b scan (stats boruvka_prof_*)
@@ -953,10 +912,6 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
     if (lane == 0) stk[0] = ((bvh.levels - 1) << 26) | 0;
     sp = 1;
     int visits = 0;
-#if HDB_LEAF_PREFETCH
-    int32_t pf_code = -1;  // stack code of the leaf held in pf
-    LeafRegs<D> pf;
-#endif
     prof.mark(0);
     while (sp > 0) {
         __builtin_amdgcn_wave_barrier();
@@ -987,33 +942,11 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
         // vector load together with the group boxes, then staged in LDS.
         n_leaf++;
         bool found = false;
-#if HDB_LEAF_PREFETCH
-        {
-            // a leaf pushes nothing, so the next pop is the entry now on top of the stack: when
-            // that is a leaf too, its loads were issued while this wave evaluated the previous
-            // leaf (one dependent round trip less per leaf run)
-            LeafRegs<D> cur;
-            if (code == pf_code)
-                cur = pf;
-            else
-                leaf_issue<D>(recs, n, bvh, idx, lane, cur);
-            leaf_commit<D>(cur, cand, bxs, bxt, lane);
-            pf_code = -1;
-            if (sp > 0) {
-                const int32_t nc = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
-                if ((nc >> 26) == 0) {
-                    leaf_issue<D>(recs, n, bvh, nc & ((1 << 26) - 1), lane, pf);
-                    pf_code = nc;
-                }
-            }
-        }
-#else
         const LRec<D> mine = fetch_rec<D>(recs, n, idx * BT + lane);
         stage_boxes<D, NSG>(bvh.slo + idx * NSG * D, bvh.shi + idx * NSG * D, bvh.stag + idx * NSG, NSG, bxs, bxt,
                             lane);
         cand[lane] = mine;  // staged now: the record's registers die before the culling
         __builtin_amdgcn_wave_barrier();
-#endif
         prof.mark(5);
         auto gneeds = [&](int gi) -> bool {
             double a[D], bb[D];
@@ -1100,52 +1033,6 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
                 continue;
             }
 #endif
-#if HDB_BOR_TWOPASS
-            // Pass 1: the group's squared distances against the bound at the group's start --
-            // independent candidates, so their LDS reads and FP64 chains overlap (the one-pass
-            // loop carried the lane's best from candidate to candidate: a dependent chain of
-            // ~200 cycles per candidate at the 1-3 waves per SIMD of the early rounds).  The
-            // bound only tightens, so a candidate failing it here fails it at its turn too.
-            const double sb0 = sb;
-            unsigned hit = 0;
-#pragma unroll 8
-            for (int k = 0; k < SG; k++) {
-                const LRec<D> r = cand[q0 + k];  // uniform address -> LDS broadcast
-                double s = sq_diff(mx[0], r.x[0]);
-#pragma unroll
-                for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
-                const bool ok = need & (k < nq) & (r.comp != mcomp);
-                if (STATS) nev += ok ? 1 : 0;  // pair evaluated for a lane that needs it
-                hit |= (ok & (s <= sb0)) ? (1u << k) : 0u;  // (s <= sb0) also drops NaN
-            }
-            unsigned any_hit = hit;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) any_hit |= __shfl_xor(any_hit, o);
-            any_hit = __builtin_amdgcn_readfirstlane(any_hit);
-            // Pass 2: the exact sequential update over the hits, in candidate order (the same
-            // sequence of best edges as the one-pass loop)
-#pragma unroll 1
-            while (any_hit) {
-                const int k = __builtin_ctz(any_hit);
-                any_hit &= any_hit - 1;
-                if (!((hit >> k) & 1u)) continue;
-                const LRec<D> r = cand[q0 + k];
-                double s = sq_diff(mx[0], r.x[0]);  // recomputed: bit-identical
-#pragma unroll
-                for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
-                if (!(s <= sb)) continue;
-                double mrd = sqrt(s);  // HDBSCANStar.java:162-168 order
-                if (mcore > mrd) mrd = mcore;
-                if (r.core > mrd) mrd = r.core;
-                const int32_t lo = mid < r.id ? mid : r.id;
-                const int32_t hi = mid < r.id ? r.id : mid;
-                if (key_less(mrd, s, lo, hi, b)) {
-                    b = Best{mrd, s, lo, hi};
-                    sb = own_sb();
-                    found = true;
-                }
-            }
-#else
             const int q1 = q0 + nq;
 #pragma unroll CAND_UNROLL
             for (int qq = q0; qq < q1; qq++) {
@@ -1167,7 +1054,6 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
                     found = true;
                 }
             }
-#endif
         }
         prof.mark(7);
         if (HDB_BOR_LEAF_PUBLISH == 2) {
@@ -1725,38 +1611,14 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
         return valid & (box_lb2v<D>(mx, a, b) < buf[K - 1]);
     };
     int sp = 0;
-#if HDB_LEAF_PREFETCH && HDB_K1T_PREFETCH
-    int64_t pf_tile = -1;  // leaf held in pf (issued while the previous leaf was evaluated)
-    LeafRegs<D> pf;
-#endif
     auto scan_leaf = [&](int64_t tile, bool own) {
         // the tile's 64 records (one coalesced vector load) and group boxes (cooperative
         // staging), one round trip; the records are staged in LDS for broadcast reads
-#if HDB_LEAF_PREFETCH && HDB_K1T_PREFETCH
-        {
-            LeafRegs<D> cur;
-            if (tile == pf_tile)
-                cur = pf;
-            else
-                leaf_issue<D>(recs, n, bvh, tile, lane, cur);
-            leaf_commit<D>(cur, cand, bxs, bxt, lane);
-            // a leaf pushes nothing: when the stack top is a leaf, it is the next pop
-            pf_tile = -1;
-            if (sp > 0) {
-                const int32_t nc = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
-                if ((nc >> 26) == 0 && (nc & ((1 << 26) - 1)) != t) {
-                    pf_tile = nc & ((1 << 26) - 1);
-                    leaf_issue<D>(recs, n, bvh, pf_tile, lane, pf);
-                }
-            }
-        }
-#else
         const LRec<D> mine = fetch_rec<D>(recs, n, tile * BT + lane);
         stage_boxes<D, NSG>(bvh.slo + tile * NSG * D, bvh.shi + tile * NSG * D, bvh.stag + tile * NSG, NSG, bxs, bxt,
                             lane);
         cand[lane] = mine;  // staged now: the record's registers die before the culling
         __builtin_amdgcn_wave_barrier();
-#endif
         auto gneeds = [&](int gi) -> bool {
             double a[D], b[D];
             staged_box<D, NSG>(bxs, gi, a, b);
@@ -1823,38 +1685,6 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
                 }
             }
 #endif
-#if HDB_BOR_TWOPASS
-            // Pass 1: the group's distances against the K-th value at the group's start
-            // (independent candidates: their LDS reads and FP64 chains overlap; the K-th value
-            // only falls, so a candidate failing here is skipped by the insertion test too).
-            // Pass 2: insertions of the hits in candidate order (the same list, ties included).
-            const double thr0 = buf[K - 1];
-            unsigned hit = 0;
-#pragma unroll 8
-            for (int k = 0; k < SG; k++) {
-                const LRec<D> r = cand[q0 + k];  // uniform address -> LDS broadcast
-                double s = sq_diff(mx[0], r.x[0]);
-#pragma unroll
-                for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
-                hit |= ((q0 + k < q1) & (r.id != skip_self) & (s < thr0)) ? (1u << k) : 0u;
-            }
-            unsigned any_hit = hit;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) any_hit |= __shfl_xor(any_hit, o);
-            any_hit = __builtin_amdgcn_readfirstlane(any_hit);
-#pragma unroll 1
-            while (any_hit) {
-                const int k = __builtin_ctz(any_hit);
-                any_hit &= any_hit - 1;
-                if (!((hit >> k) & 1u)) continue;
-                const LRec<D> r = cand[q0 + k];
-                double s = sq_diff(mx[0], r.x[0]);  // recomputed: bit-identical
-#pragma unroll
-                for (int c = 1; c < D; c++) s = s + sq_diff(mx[c], r.x[c]);
-                if (IDX) topk_insert_idx<K>(buf, bix, s, (int)(tile * BT + q0 + k));
-                else topk_insert<K>(buf, s);
-            }
-#else
 #pragma unroll CAND_UNROLL
             for (int qq = q0; qq < q1; qq++) {
                 const LRec<D> r = cand[qq];  // uniform address -> LDS broadcast
@@ -1865,7 +1695,6 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
                 if (IDX) topk_insert_idx<K>(buf, bix, s, (int)(tile * BT + qq));
                 else topk_insert<K>(buf, s);
             }
-#endif
         }
     };
     scan_leaf(t, true);  // own tile first: the K-th bound is tight from the start
@@ -2087,12 +1916,15 @@ bool knn_tree_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC, bo
 // ------------------------------------------------------------------- K2b host
 // per-round Boruvka state carved after the index: comp_w, comp_key, comp_s, best_w, best_s
 // (8n each), best_lo/hi, parent, parent2 (4n each), counters, edge lists
-static size_t boruvka_extra_bytes(int64_t n) {
+// diag: count_evals -- one BOR_STATS_REC-word record per scan wave, sized for the most waves a
+// round can have (16 points per wave: boruvka_wave_pts / boruvka_early_pts may ask for it)
+static size_t boruvka_extra_bytes(int64_t n, bool diag) {
     const size_t per = (size_t)n;
     auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t waves_max = (size_t)ceil_div(n, (int64_t)WGRP) * (WGRP / 16);
     return 5 * rnd(8 * per) + 5 * rnd(4 * per) + 3 * 256 + 2 * rnd(4 * per) + rnd(8 * per) +
-           rnd(8 * (per / 16 + 72)) +  // + diagnostics: counters and per-wave cycles (count_evals)
-           rnd(4 * per) + 3 * rnd(4 * (per / WGRP + 1)) + rnd(8 * (per / 16 + 64)) + 256 +  // + work lists
+           (diag ? rnd(8 * (size_t)BOR_STATS_REC * waves_max) : 0) +
+           rnd(4 * per) + 3 * rnd(4 * (per / WGRP + 1)) + rnd(8 * waves_max) + 256 +  // + work lists
            2 * rnd(4 * per) + rnd(8 * per) + rnd(per);  // + best_pos, pcomp, lbw, xact
 }
 
@@ -2148,7 +1980,7 @@ static void boruvka_impl(hdb_ctx *ctx, const double *X, int64_t n, const double 
     Carve cv;
     char *extra = nullptr;
     KernelTimer tt(ctx, "boruvka_total");
-    Spatial<D> sp = build_spatial_in<D>(ctx, A_WORK0, X, n, core, cv, boruvka_extra_bytes(n), &extra);
+    Spatial<D> sp = build_spatial_in<D>(ctx, A_WORK0, X, n, core, cv, boruvka_extra_bytes(n, ctx->count_evals), &extra);
     boruvka_on_index<D>(ctx, sp, n, extra, nullptr, va, vb, w);
 }
 
@@ -2182,6 +2014,8 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
     unsigned long long *desc = ex.take<unsigned long long>(max_waves);
     int32_t *nwaves = ex.take<int32_t>(1);
     unsigned long long *evals = ctx->count_evals ? ex.take<unsigned long long>((size_t)BOR_STATS_REC * max_waves) : nullptr;
+    if (ex.off > boruvka_extra_bytes(n, ctx->count_evals))
+        HDB_THROW(HDB_EINVAL, "boruvka: scratch carve exceeds its reserve");
     int64_t tot_evals = 0;
     Rec<D> *recs = sp.recs;
     int32_t *inv = sp.inv;
@@ -2432,7 +2266,7 @@ static void exact_leaf_impl(hdb_ctx *ctx, const double *X, int64_t n, int min_pt
                             int self_edges, int32_t *va, int32_t *vb, double *w) {
     KernelTimer tt(ctx, "exact_leaf_total");
     auto rnd = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t bx = rnd(boruvka_extra_bytes(n));
+    const size_t bx = rnd(boruvka_extra_bytes(n, ctx->count_evals));
     const size_t nk = (size_t)n * K;
     const size_t more = rnd(8 * nk) + rnd(4 * nk) + rnd(8 * nk) + rnd((size_t)n) + 256;
     Carve cv;

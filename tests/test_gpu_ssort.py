@@ -4,7 +4,7 @@ path it replaces (ctx option ssort=0) and the oracle, bit for bit.
 * hdb_sort_edges_desc (the reducers' stable descending merge, SortMST.java:9-17 over
   UnionFindReducer.java:19-69) against oracle.merge_edges: sizes on both sides of every
   plan boundary (one workgroup, 2..4096 buckets), heavy and total ties, -0.0 next to +0.0,
-  presorted and reversed inputs, NaN/inf, and the forced chunked-merge path (ssort_cap);
+  presorted and reversed inputs, +-inf and huge magnitudes, and the forced chunked-merge path (ssort_cap);
 * hdb_exact_mst (the Morton order of the index, the tree/self edge orders of both output
   modes) and K6 flat labels (the stability terms' order) with ssort on and off: identical.
 """

@@ -27,7 +27,8 @@ def eq(a, b):
 @contextlib.contextmanager
 def options(ctx, **kw):
     defaults = {"knn_tree": 1, "knn_tree_min_n": 8192, "knn_fp32_screen": 1, "count_evals": 0,
-                "leaf_seed_k": -1, "leaf_list_rounds": 2, "boruvka_seed": 1}
+                "leaf_seed_k": -1, "leaf_list_rounds": 2, "boruvka_seed": 1, "boruvka_wave_pts": 64,
+                "boruvka_early_pts": 0}
     try:
         for k, v in kw.items():
             ctx.set_option(k, v)
@@ -201,7 +202,11 @@ def test_exact_mst_seeding_options_equal(ctx, star, d):
     ref = _sorted_edges(star.constructMSTBoruvka(X, core, False))
     for kw in ({}, dict(leaf_seed_k=0), dict(leaf_seed_k=7, leaf_list_rounds=64),
                dict(leaf_seed_k=15, leaf_list_rounds=1), dict(leaf_list_rounds=0),
-               dict(boruvka_seed=0), dict(boruvka_seed=0, leaf_list_rounds=1)):
+               dict(boruvka_seed=0), dict(boruvka_seed=0, leaf_list_rounds=1),
+               # the diagnostic pass at its largest per-wave record count (the
+               # record buffer must fit its carve at 16 points per wave)
+               dict(count_evals=1, boruvka_wave_pts=16, boruvka_early_pts=16),
+               dict(count_evals=1, boruvka_wave_pts=32)):
         with options(ctx, **kw):
             c2, g = star.exactMST(X, 4, None, 2, selfEdges=False)
         assert eq(c2, core), kw
