@@ -90,7 +90,11 @@ struct hdb_ctx {
     bool merge_runs = false;   // merge sort: radix-sort only what follows a non-decreasing prefix, then merge (slower as built: sync + binary searches)
     int flat_link_variant = 1;  // K6 dc_link A/B: 0 direct guarded atomics, 1 LDS-combined multi-batch
     int flat_root_variant = 3;  // K6 dc_root A/B: 0 LDS table (256 threads), 1 (1024), 2 direct atomics, 3-5 multi-batch
-    int flat_block_log = 10;   // K6: deep depths per workgroup in LDS (2^x ranks, 8-10; 0: the sequential dc_local)
+    bool flat_relabel = true;  // K6: divide-and-conquer vertex labels in rank order (locality; false: point ids)
+    int flat_block_log = 10;
+    int flat_deep_depth = 64;  // K6: global depths >= this use flat_deep_root / flat_deep_link (A/B)
+    int flat_deep_root = 3;
+    int flat_deep_link = 1;   // K6: deep depths per workgroup in LDS (2^x ranks, 8-10; 0: the sequential dc_local)
     bool ssort = true;         // sample sort (ssort.hpp) for the Morton order, the edge orders and K6's term sort
                                // (false: the rocPRIM radix chains; A/B and tests)
     int ssort_cap = 0;         // ssort bucket size sorted in LDS (0: SS_CAP; tests lower it to run the merge path)

@@ -176,6 +176,10 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         if (const char *e = getenv("HDB_FLAT_ROOT")) c->flat_root_variant = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_MERGE_RUNS")) c->merge_runs = atoi(e) != 0;      // A/B knob
         if (const char *e = getenv("HDB_SSORT")) c->ssort = atoi(e) != 0;                // A/B knob
+        if (const char *e = getenv("HDB_FLAT_RELABEL")) c->flat_relabel = atoi(e) != 0;  // A/B knob
+        if (const char *e = getenv("HDB_FLAT_DEEP")) c->flat_deep_depth = atoi(e);          // A/B knob
+        if (const char *e = getenv("HDB_FLAT_DEEP_ROOT")) c->flat_deep_root = atoi(e);      // A/B knob
+        if (const char *e = getenv("HDB_FLAT_DEEP_LINK")) c->flat_deep_link = atoi(e);      // A/B knob
         *out = c;
         return HDB_OK;
     } catch (const Error &e) {
@@ -357,6 +361,10 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
     }
     if (k == "boruvka_knn_seed") {
         ctx->boruvka_knn_seed = value != 0;
+        return HDB_OK;
+    }
+    if (k == "flat_relabel") {
+        ctx->flat_relabel = value != 0;
         return HDB_OK;
     }
     if (k == "ssort") {

@@ -201,6 +201,30 @@ __global__ void fl_point_parent(const int32_t *__restrict__ ea, const int32_t *_
     }
 }
 
+// Vertex labels for the divide and conquer ordered by rank (locality): point v becomes
+// 2 pp(v) + side, pp(v) = its lightest edge (rank) and side = 1 when v is that edge's second
+// endpoint -- unique, < 2m.  A block of ranks [lo, hi) then touches the records of labels near
+// [2lo, 2hi) for most of its vertices instead of points scattered over all n ids.
+__global__ void fl_relabel_orig(const int32_t *__restrict__ pparent, const int32_t *__restrict__ eb, int64_t n,
+                                int32_t *__restrict__ orig) {
+    HDB_GRID_STRIDE(v, n) {
+        const int32_t p = pparent[v];
+        if (p == NONE) continue;  // a point no edge touches (malformed input: the union-find reports it)
+        orig[2 * (int64_t)p + (eb[p] == (int32_t)v ? 1 : 0)] = (int32_t)v;
+    }
+}
+__global__ void fl_relabel(const int32_t *__restrict__ ea, const int32_t *__restrict__ eb,
+                           const int32_t *__restrict__ pparent, int64_t m, int32_t *__restrict__ lab) {
+    HDB_GRID_STRIDE(r, m) {
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const int32_t v = s ? eb[r] : ea[r];
+            const int32_t p = pparent[v];
+            lab[2 * r + s] = 2 * p + (eb[p] == v ? 1 : 0);
+        }
+    }
+}
+
 // ------------------------------------------------------- 2. Kruskal tree, depth kernels
 // L edge #i of depth bit b: rank with bit b clear
 __device__ __forceinline__ int64_t l_rank(int64_t i, int b) {
@@ -215,8 +239,10 @@ struct DC {
     int32_t *parent;    // m: parent edge rank (NONE: root)
     int32_t *esize;     // m: |C(e)|
     int32_t *eminid;    // m: smallest point id in C(e)
-    int64_t n, m;
+    const int32_t *orig;  // vertex label -> point id (nullptr: the label is the point id)
+    int64_t n, m;         // n: vertex labels (contracted labels are n + root edge rank)
 };
+__device__ __forceinline__ int32_t vid(const DC &c, int32_t x) { return c.orig ? c.orig[x] : x; }
 
 __global__ void dc_init(DC c, int b, int j, int64_t nl) {
     HDB_GRID_STRIDE(i, nl) {
@@ -281,7 +307,7 @@ __global__ __launch_bounds__(TB) void dc_root(DC c, int b, int j, int64_t nl) {
             const int32_t x = c.hooked[r];
             c.hooked[r] = rep;  // dc_link reads the representative back instead of a second find
             const int32_t sz = x < 0 ? 0 : (x < c.n ? 1 : c.esize[x - c.n]);
-            const int32_t mi = x < 0 ? NONE : (x < c.n ? x : c.eminid[x - c.n]);
+            const int32_t mi = x < 0 ? NONE : (x < c.n ? vid(c, x) : c.eminid[x - c.n]);
             uint32_t h = uf_prio(rep, 0) & (SLOTS - 1);
             while (true) {  // <= TB distinct keys in 2x slots: always finds one
                 int32_t k = atomicCAS(&skey[h], -1, rep);
@@ -342,7 +368,7 @@ __global__ __launch_bounds__(TB) void dc_root_multi(DC c, int b, int j, int64_t 
                 const int32_t x = c.hooked[r];
                 c.hooked[r] = rep;
                 const int32_t sz = x < 0 ? 0 : (x < c.n ? 1 : c.esize[x - c.n]);
-                const int32_t mi = x < 0 ? NONE : (x < c.n ? x : c.eminid[x - c.n]);
+                const int32_t mi = x < 0 ? NONE : (x < c.n ? vid(c, x) : c.eminid[x - c.n]);
                 uint32_t h = uf_prio(rep, 0) & (SLOTS - 1);
                 while (true) {  // the table is kept below SLOTS - TB keys before every batch
                     const int32_t k = atomicCAS(&skey[h], -1, rep);
@@ -381,7 +407,7 @@ __global__ void dc_root_direct(DC c, int b, int j, int64_t nl) {
         atomicMax(&c.lr[rep].rootedge, (int32_t)r);
         if (x >= 0) {
             atomicAdd(&c.lr[rep].csize, x < c.n ? 1 : c.esize[x - c.n]);
-            atomicMin(&c.lr[rep].cmin, x < c.n ? x : c.eminid[x - c.n]);
+            atomicMin(&c.lr[rep].cmin, x < c.n ? vid(c, x) : c.eminid[x - c.n]);
         }
     }
 }
@@ -395,7 +421,7 @@ __global__ void dc_link(DC c, int b, int j, int64_t nl) {
             const LRec q = c.lr[rep];
             if (q.rootedge == (int32_t)r) {
                 c.esize[r] = q.csize + (rep < c.n ? 1 : c.esize[rep - c.n]);
-                c.eminid[r] = min(q.cmin, rep < c.n ? rep : c.eminid[rep - c.n]);
+                c.eminid[r] = min(q.cmin, rep < c.n ? vid(c, rep) : c.eminid[rep - c.n]);
             }
         }
         const int64_t u = r | (int64_t(1) << b);  // the U edge paired with this thread
@@ -448,7 +474,7 @@ __global__ __launch_bounds__(TB) void dc_link_multi(DC c, int b, int j, int64_t 
                     const LRec q = c.lr[rep];
                     if (q.rootedge == (int32_t)r) {
                         c.esize[r] = q.csize + (rep < c.n ? 1 : c.esize[rep - c.n]);
-                        c.eminid[r] = min(q.cmin, rep < c.n ? rep : c.eminid[rep - c.n]);
+                        c.eminid[r] = min(q.cmin, rep < c.n ? vid(c, rep) : c.eminid[rep - c.n]);
                     }
                 }
                 const int64_t u = r | (int64_t(1) << b);
@@ -539,7 +565,7 @@ __global__ __launch_bounds__(TB) void dc_block(DC c, int *__restrict__ err) {
                 const int32_t old = atomicCAS(&key[h], -1, x);
                 if (old == -1) {
                     bsz[h] = x < c.n ? 1 : c.esize[x - c.n];
-                    bmn[h] = x < c.n ? x : c.eminid[x - c.n];
+                    bmn[h] = x < c.n ? vid(c, x) : c.eminid[x - c.n];
                     break;
                 }
                 if (old == x) break;
@@ -659,7 +685,7 @@ __global__ __launch_bounds__(64) void dc_local(DC c, int *__restrict__ err) {
                     luf[h] = (int16_t)h;
                     lre[h] = -1;
                     lsz[h] = x < c.n ? 1 : c.esize[x - c.n];
-                    lmn[h] = x < c.n ? x : c.eminid[x - c.n];
+                    lmn[h] = x < c.n ? vid(c, x) : c.eminid[x - c.n];
                     break;
                 }
                 if (old == x) break;
@@ -1376,6 +1402,9 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     const int64_t m = n - 1;  // a spanning tree has exactly n - 1 non-self edges
     int64_t *pin = pinned_words(ctx) + PINNED_WORDS - 8;  // private slice
     const int64_t mm = std::max<int64_t>(m, 1);
+    // vertex labels of the divide and conquer: rank-ordered (2m of them) or the point ids
+    const bool relabel = ctx->flat_relabel && m >= 1;
+    const int64_t nv = relabel ? 2 * mm : n;
 
     // scratch: sizes are fixed by n and ne
     auto layout = [&](Carver &cv) {
@@ -1389,8 +1418,9 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         cv.take<int32_t>(mm);            // eb
         cv.take<double>(mm);             // ew
         cv.take<int32_t>(2 * mm);        // lab
-        cv.take<LRec>(n + mm);           // label records
-        cv.take<int32_t>(n + mm);        // stamp
+        cv.take<LRec>(nv + mm);          // label records
+        cv.take<int32_t>(nv + mm);       // stamp
+        cv.take<int32_t>(nv);            // orig (relabelled vertices)
         cv.take<int32_t>(mm);            // hooked
         for (int k = 0; k < 3; k++) cv.take<int32_t>(mm);      // parent esize eminid
         cv.take<int32_t>(n);             // pparent
@@ -1408,15 +1438,17 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     double *ew = cv.take<double>(mm);
     DC dc;
     dc.lab = cv.take<int32_t>(2 * mm);
-    dc.lr = cv.take<LRec>(n + mm);
-    dc.stamp = cv.take<int32_t>(n + mm);
+    dc.lr = cv.take<LRec>(nv + mm);
+    dc.stamp = cv.take<int32_t>(nv + mm);
+    int32_t *orig = cv.take<int32_t>(nv);
     dc.hooked = cv.take<int32_t>(mm);
     dc.parent = cv.take<int32_t>(mm);
     dc.esize = cv.take<int32_t>(mm);
     dc.eminid = cv.take<int32_t>(mm);
     int32_t *pparent = cv.take<int32_t>(n);
-    dc.n = n;
+    dc.n = nv;
     dc.m = m;
+    dc.orig = relabel ? orig : nullptr;
 
     HIP_CHECK(hipMemsetAsync(words, 0, sizeof(int64_t) * 4, st));
     // ---- 1. compact, validate, order
@@ -1465,9 +1497,13 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         perm = i2;
     }
     hipLaunchKernelGGL(fl_rank, dim3(g), dim3(256), 0, st, ca, cb, cw, m, desc, perm, ea, eb, ew, dc.lab, dc.parent);
-    hipLaunchKernelGGL(fill_i32, dim3(grid_for(n + m)), dim3(256), 0, st, dc.stamp, n + m, -1);
+    hipLaunchKernelGGL(fill_i32, dim3(grid_for(nv + m)), dim3(256), 0, st, dc.stamp, nv + m, -1);
     hipLaunchKernelGGL(fill_i32, dim3(grid_for(n)), dim3(256), 0, st, pparent, n, NONE);
     hipLaunchKernelGGL(fl_point_parent, dim3(g), dim3(256), 0, st, ea, eb, m, pparent);
+    if (relabel) {
+        hipLaunchKernelGGL(fl_relabel_orig, dim3(grid_for(n)), dim3(256), 0, st, pparent, eb, n, orig);
+        hipLaunchKernelGGL(fl_relabel, dim3(g), dim3(256), 0, st, ea, eb, pparent, m, dc.lab);
+    }
 
     // ---- 2. Kruskal tree by rank divide and conquer
     int J = 0;
@@ -1482,7 +1518,10 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         const int gl = grid_for(nl);
         hipLaunchKernelGGL(dc_init, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
         hipLaunchKernelGGL(dc_unite, dim3(gl), dim3(256), 0, st, dc, b, nl, err);
-        switch (ctx->flat_root_variant) {
+        // deep depths: small components, no hot records -- the per-workgroup LDS tables only
+        // cost occupancy (the multi-batch kernels run nl / 4096 workgroups)
+        const bool deep = j >= ctx->flat_deep_depth;
+        switch (deep ? ctx->flat_deep_root : ctx->flat_root_variant) {
         case 1: hipLaunchKernelGGL((dc_root<1024, 4096>), dim3((unsigned)ceil_div(nl, 1024)), dim3(1024), 0, st, dc, b, j, nl); break;
         case 2: hipLaunchKernelGGL(dc_root_direct, dim3(gl), dim3(256), 0, st, dc, b, j, nl); break;
         case 3: hipLaunchKernelGGL((dc_root_multi<1024, 4096, 4>), dim3((unsigned)ceil_div(nl, 4096)), dim3(1024), 0, st, dc, b, j, nl); break;
@@ -1490,7 +1529,7 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         case 5: hipLaunchKernelGGL((dc_root_multi<512, 4096, 4>), dim3((unsigned)ceil_div(nl, 2048)), dim3(512), 0, st, dc, b, j, nl); break;
         default: hipLaunchKernelGGL((dc_root<ROOT_TB, ROOT_SLOTS>), dim3(gl), dim3(ROOT_TB), 0, st, dc, b, j, nl);
         }
-        if (ctx->flat_link_variant == 1)
+        if ((deep ? ctx->flat_deep_link : ctx->flat_link_variant) == 1)
             hipLaunchKernelGGL((dc_link_multi<1024, 8192, 2>), dim3((unsigned)ceil_div(nl, 2048)), dim3(1024), 0, st, dc,
                                b, j, nl);
         else

@@ -176,3 +176,25 @@ def test_device_long_chains_equal_host(pkg, ctx, shape):
         ref, kr = lib_flat(pkg, va[d], vb[d], w[d], n, mcs)
         got, kg = dev_flat(pkg, ctx, va[d], vb[d], w[d], n, mcs)
         assert kg == kr and np.array_equal(got, ref), (shape, mcs)
+
+
+@pytest.mark.parametrize("relabel", [0, 1])
+@pytest.mark.parametrize("n,wmax", [(5000, 3), (200_000, None)])
+def test_device_vertex_relabel_either_way(pkg, ctx, relabel, n, wmax):
+    """the divide and conquer's rank-ordered vertex labels (flat_relabel, default on) and the
+    point-id labels give the host algorithm's labels"""
+    rng = np.random.default_rng(n + 1)
+    par = (rng.random(n - 1) * np.arange(1, n)).astype(np.int64)
+    va, vb = par.astype(np.int32), np.arange(1, n, dtype=np.int32)
+    w = rng.random(n - 1) if wmax is None else rng.integers(0, wmax + 1, n - 1).astype(np.float64)
+    perm = rng.permutation(n).astype(np.int32)
+    va, vb = perm[va], perm[vb]
+    d = np.argsort(-w, kind="stable")
+    ctx.set_option("flat_relabel", relabel)
+    try:
+        for mcs in (2, 5):
+            ref, kr = lib_flat(pkg, va[d], vb[d], w[d], n, mcs)
+            got, kg = dev_flat(pkg, ctx, va[d], vb[d], w[d], n, mcs)
+            assert kg == kr and np.array_equal(got, ref), (n, wmax, mcs, relabel)
+    finally:
+        ctx.set_option("flat_relabel", 1)
