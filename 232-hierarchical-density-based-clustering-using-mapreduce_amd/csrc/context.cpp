@@ -325,7 +325,7 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
         return HDB_OK;
     }
     if (k == "prim_coop_slots") {
-        if (value < 0 || value > 5) return HDB_EINVAL;
+        if (value < 0 || value > 6) return HDB_EINVAL;
         ctx->prim_coop_slots = (int)value;
         return HDB_OK;
     }

@@ -1230,6 +1230,628 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
     }
 }
 
+// ------------------------------------------ cooperative kernel, speculative steps (slots 6)
+// The same Prim (HDBSCANStar.java:124-205 / HdbscanDataBubbles.java:165-254: select the
+// unattached vertex with the smallest best, ties -> largest index; update iff mrd < best,
+// parent = the vertex just attached), with many steps per exchange instead of one.
+//
+// A round starts from an exact state.  Every workgroup publishes its C = 64 / nwg best
+// unattached vertices (each wave's best two, the workgroup's best C of those) with their rows;
+// the union is the round's list L (<= 64 vertices), known to every workgroup.  Then every wave
+// runs the Prim on its own, without barriers or exchanges: step t takes the best unattached
+// member of L (its key is tracked redundantly by every wave: lane j holds member j's row and
+// relaxes it exactly as the owning lane does, so the keys agree bit for bit), every lane relaxes
+// against it, and the wave checks its own lanes: if a non-member of L beats the step's pick
+// ((best, index) order of the select rule), step t is where the round's picks stop being the
+// Prim's, and the wave stops.  One exchange then gives s* = the first such step over all waves
+// and the true vertex of step s* (the best violating vertex of the waves that stop there).
+// Steps < s* were the Prim's own; every lane undoes the speculation past them (a lane whose
+// last improvement came at a step >= s* restores its round-start best/parent and re-relaxes
+// against the picks of steps < s*; a vertex attached at a step >= s* is detached), attaches the
+// true vertex of step s* and relaxes against it.  The result is the sequential Prim's state
+// after s* + 1 steps, so the output is the reference's whatever the speculation did.  The list
+// only decides how many steps a round commits (simulated on 16,384 8-d blob points: ~34).
+// LDS hand-off between the waves of one workgroup without waiting for global loads in flight
+// (a release/acquire atomic also waits for vmcnt): the writer waits for its own LDS operations
+// only (s_waitcnt lgkmcnt(0)) before the flag store; the reader's compiler barrier keeps the
+// payload loads behind the flag load, and LDS serves them after it
+__device__ __forceinline__ void lds_publish(int *flag, int v) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0); vmcnt, expcnt untouched
+    __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int lds_peek(int *flag) {
+    const int v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    return v;
+}
+
+template <int BS, int DM>
+__global__ __launch_bounds__(BS + 64) void prim_spec_kernel(PrimIn in, int n, int self_edges, int32_t *__restrict__ va,
+                                                       int32_t *__restrict__ vb, double *__restrict__ w,
+                                                       gu64 *__restrict__ gcand, gu64 *__restrict__ gviol, int *err,
+                                                       unsigned spin_limit, int spread, int *__restrict__ xcc,
+                                                       int res, unsigned long long *__restrict__ stats,
+                                                       unsigned *__restrict__ gstop) {
+    if ((int)(blockIdx.x % spread) != res) return;  // an idle block of a spread grid
+    // wave 0 leads (the list, the picks) and owns no vertex; waves 1 .. BS/64 one vertex per lane
+    constexpr int NW = BS / 64 + 1;
+    constexpr int ND = DM + 3;       // x, core, eB, nnB
+    constexpr int GC = 3;            // candidate granules: key lo, key hi, index (rows: read from X by index)
+    constexpr int GV = 4;            // violation granules: step, key lo, key hi, index
+    constexpr unsigned long long KINF = 0x7ff0000000000000ull;  // key of +inf: nothing to offer
+    const int nwg = (int)gridDim.x / spread;
+    const int bid = (int)blockIdx.x / spread;
+    const int C = min(64 / nwg, 2 * NW);  // list entries per workgroup (nwg <= 64)
+    const int NL = C * nwg;          // list size
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int i = tid < 64 ? n + tid : bid * BS + tid - 64;  // the leader's lanes: no vertex (>= n)
+
+    __shared__ unsigned long long s_wck[NW * 2];  // ... keys
+    __shared__ int s_wci[NW * 2];                 // ... indices
+    __shared__ unsigned s_cg[64 * GC];            // swept candidate granules (values)
+    __shared__ double s_lrow[64][ND];             // the list: rows, keys, indices
+    __shared__ double s_lkey[64];
+    __shared__ int s_lidx[64];
+    __shared__ int s_inl[BS + 64];                // round tag: this lane's vertex is a list member
+    __shared__ int s_pick[65];                    // wave 0's picks (list entry per step)
+    __shared__ int s_vt[NW];                      // per wave: first violating step
+    __shared__ unsigned long long s_vk[NW];       // ... its best violating vertex: key, index, row
+    __shared__ int s_vi[NW];
+    __shared__ unsigned s_vg[64 * GV];            // swept violation granules (values)
+    __shared__ double s_wrow[ND];                 // the round's true vertex at s*: row
+    __shared__ int s_star, s_win, s_local, s_stop;
+    __shared__ int s_sel[64];
+    __shared__ int s_vmin;                        // this round's first violating step in the workgroup
+    __shared__ unsigned long long s_pkey[65];     // wave 0's picks: key, index; published step count
+    __shared__ int s_pidx[65];
+    __shared__ int s_tick, s_lstop;
+
+    if (tid == 0) s_local = 0;
+    if (spread > 1 && wid == 0) {  // every working block on one XCC?  (as prim_coop4_kernel)
+        if (lane == 0) {
+            unsigned x;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+            __hip_atomic_store(xcc + bid, (int)(x & 15u) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bool same = true;
+        int first = 0;
+        for (unsigned spins = 0;;) {
+            bool ok = true;
+            int mn = 1 << 30, mx = -1;
+            for (int j = lane; j < nwg; j += 64) {
+                const int v = __hip_atomic_load(xcc + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok &= v != 0;
+                mn = min(mn, v);
+                mx = max(mx, v);
+            }
+            if (__all(ok)) {
+                for (int o = 32; o >= 1; o >>= 1) {
+                    mn = min(mn, __shfl_xor(mn, o));
+                    mx = max(mx, __shfl_xor(mx, o));
+                }
+                same = mn == mx;
+                first = mn;
+                break;
+            }
+            if (++spins > spin_limit) {
+                if (lane == 0) atomicExch(err, 1);
+                first = -1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (lane == 0) s_local = first < 0 ? -1 : (same && first > 0);
+    }
+    s_inl[tid] = 0;
+    __syncthreads();
+    if (s_local < 0) return;
+    const bool local = s_local != 0;
+
+    // own row and state
+    double xi[DM], ci = 0, ebi = 0, nni = 0;
+#pragma unroll
+    for (int c = 0; c < DM; c++) xi[c] = (i < n && c < in.d) ? in.X[(int64_t)i * in.d + c] : 0.0;
+    if (i < n) {
+        ci = in.core[i];
+        if (in.eB) {
+            ebi = in.eB[i];
+            nni = in.nnB[i];
+        }
+    }
+    double best = JMAX;
+    int par = -1;
+    bool att = (i >= n) || (i == n - 1);
+    {  // the start vertex n - 1
+        double xc[DM];
+#pragma unroll
+        for (int c = 0; c < DM; c++) xc[c] = c < in.d ? in.X[(int64_t)(n - 1) * in.d + c] : 0.0;
+        const double cc = in.core[n - 1], ebc = in.eB ? in.eB[n - 1] : 0.0, nnc = in.eB ? in.nnB[n - 1] : 0.0;
+        if (!att) {
+            bool imp = false;
+            const double mrd = coop_mrd<DM>(in, xc, cc, ebc, nnc, xi, ci, ebi, nni, best, imp);
+            if (imp) {
+                best = mrd;
+                par = n - 1;
+            }
+        }
+    }
+    auto put = [&](gu64 *dst, unsigned tag, unsigned val) {
+        const unsigned long long gv = ((unsigned long long)tag << 32) | val;
+        if (local)
+            __hip_atomic_store(dst, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+            __hip_atomic_store(dst, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // wave 0: read `count` granules at src until every tag is `tag`, values to dst (LDS)
+    auto sweep = [&](const gu64 *src, int count, unsigned tag, unsigned *dst) -> bool {
+        for (unsigned spins = 0;;) {
+            bool ok = true;
+            for (int b = 0; b < count; b += 64 * 8) {  // 8 loads in flight per lane, then one wait
+                unsigned long long x[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int j = b + k * 64 + lane;
+                    x[k] = j < count ? __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : ((unsigned long long)tag << 32);
+                }
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int j = b + k * 64 + lane;
+                    ok &= (unsigned)(x[k] >> 32) == tag;
+                    if (j < count) dst[j] = (unsigned)x[k];
+                }
+            }
+            if (__all(ok)) return true;
+            if (++spins > spin_limit) {
+                if (lane == 0) atomicExch(err, 1);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    };
+
+    int committed = 0;  // Prim steps done (vertices attached after n - 1)
+    unsigned long long n_rounds = 0, n_spec = 0, cyc[4] = {0, 0, 0, 0}, n_exec = 0;
+    unsigned long long tm = __builtin_amdgcn_s_memtime();
+    auto tick = [&](int k) {  // per-phase cycles of workgroup 0, thread 0 (prim_spec_cyc_* stats)
+        if (tid == 0) {
+            const unsigned long long x = __builtin_amdgcn_s_memtime();
+            cyc[k] += x - tm;
+            tm = x;
+        }
+    };
+    for (unsigned round = 1; committed < n - 1; round++) {
+        const int buf = round & 1;
+        // ---- 1. the list: each wave's two best, the workgroup's best C, every workgroup's C
+        {
+            unsigned long long key = att ? KINF : mrd_key(best);
+            const unsigned long long k1 = wave_min_u64(key);
+            const int l1 = last_lane(key == k1);  // lanes grow with the vertex index: largest index
+            const unsigned long long key2 = lane == l1 ? KINF : key;
+            const unsigned long long k2 = wave_min_u64(key2);
+            const int l2 = last_lane(key2 == k2);
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                const int lq = q ? l2 : l1;
+                const unsigned long long kq = q ? k2 : k1;
+                if (lane == lq) {
+                    s_wck[2 * wid + q] = kq;
+                    s_wci[2 * wid + q] = kq < KINF ? i : -1;
+                }
+            }
+        }
+        __syncthreads();
+        if (wid == 0) {
+            // the workgroup's best C of its 2 NW wave candidates (lane q < 2 NW holds candidate q)
+            unsigned long long qk = lane < 2 * NW ? s_wck[lane] : KINF;
+            const int qi = lane < 2 * NW ? s_wci[lane] : -1;
+            if (qi < 0) qk = KINF;
+            int sel = -1;  // lane e < C: the candidate (lane) ranked e
+            for (int e = 0; e < C; e++) {
+                const unsigned long long m = wave_min_u64(qk);
+                int pick = -1;
+                if (m < KINF) {  // largest index among the minima
+                    const unsigned long long inv = (qk == m) ? (0xffffffffull - (unsigned)qi) : ~0ull;
+                    const unsigned long long mi = wave_min_u64(inv);
+                    pick = last_lane(inv == mi && qk == m);
+                }
+                if (lane == e) sel = pick;
+                if (pick >= 0 && lane == pick) qk = KINF;
+            }
+            s_sel[lane] = sel;
+            __builtin_amdgcn_wave_barrier();
+            // publish: entry e's granules at [e * GC, (e + 1) * GC)
+            gu64 *dst = gcand + ((size_t)buf * nwg + bid) * (size_t)(C * GC);
+            for (int g = lane; g < C * GC; g += 64) {
+                const int e = g / GC, f = g - e * GC;
+                const int q = s_sel[e];
+                unsigned val;
+                if (q < 0) val = f == 2 ? 0xffffffffu : 0u;
+                else if (f < 2) val = (unsigned)(s_wck[q] >> (32 * f));
+                else val = (unsigned)s_wci[q];
+                put(dst + g, round, val);
+            }
+            // sweep every workgroup's entries
+            const bool ok = sweep(gcand + (size_t)buf * nwg * (size_t)(C * GC), NL * GC, round, s_cg);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) {
+                s_vmin = 1 << 30;
+                s_tick = 0;
+                s_lstop = 1 << 30;
+            }
+            if (!ok) {
+                if (lane == 0) s_stop = 1;
+            } else {
+                if (lane == 0) s_stop = 0;
+                // list entry j = lane (j < NL): key, index, row into LDS
+                if (lane < NL) {
+                    const unsigned *g = s_cg + lane * GC;
+                    const int li = (int)g[2];
+                    s_lidx[lane] = li;
+                    s_lkey[lane] = __longlong_as_double((long long)(((unsigned long long)g[1] << 32) | g[0]));
+                    if (li >= 0) {  // the member's row, as its owning lane holds it
+#pragma unroll
+                        for (int c = 0; c < DM; c++) s_lrow[lane][c] = c < in.d ? in.X[(int64_t)li * in.d + c] : 0.0;
+                        s_lrow[lane][DM] = in.core[li];
+                        s_lrow[lane][DM + 1] = in.eB ? in.eB[li] : 0.0;
+                        s_lrow[lane][DM + 2] = in.eB ? in.nnB[li] : 0.0;
+                    }
+                    if (li >= 0 && li / BS == bid) s_inl[li % BS + 64] = (int)round;
+                } else if (lane < 64) {
+                    s_lidx[lane] = -1;
+                }
+            }
+        }
+        __syncthreads();
+        if (s_stop) break;  // a timed-out sweep (not co-resident): reported through err
+        tick(0);
+        const bool inl = s_inl[tid] == (int)round;
+
+        // ---- 2. speculation.  Wave 0 tracks the list (lane j: member j's row and key) and
+        // publishes each step's pick (s_pick / s_pkey / s_pidx, then the step count s_tick with
+        // release order); every wave checks and relaxes its own lanes against the published picks
+        // and stops at its first violation, or once the workgroup's (LDS) or anyone's (global)
+        // first violation lies behind it.
+        double lx[DM], lc = 0.0, le = 0.0, ln = 0.0, lk = 0.0;
+        int li = -1;
+        bool latt = true;
+        if (wid == 0) {
+#pragma unroll
+            for (int c = 0; c < DM; c++) lx[c] = s_lrow[lane][c];
+            lc = s_lrow[lane][DM];
+            le = s_lrow[lane][DM + 1];
+            ln = s_lrow[lane][DM + 2];
+            lk = s_lkey[lane];
+            li = s_lidx[lane];
+            latt = li < 0;
+        }
+        const double best0 = best;
+        const int par0 = par;
+        double b2 = best;  // the value before the last improvement of this round (t2: its step)
+        int p2 = par, t2 = -1, tstep = -1, astep = 1 << 30;
+        // the first violating step anyone found this round: in this workgroup (LDS) or in any
+        // (a global word min-combined as (rounds left, step): a newer round always wins), the
+        // global word read 4 steps ahead so its latency overlaps the steps in between
+        const unsigned rtag = (0xffffffu - round) << 7;
+        unsigned gpre = __hip_atomic_load(gstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int gs = 1 << 30;
+        for (int t = 0;; t++) {
+            bool stop = false;
+            if (t > 0) {
+                if ((t & 3) == 0) {
+                    gs = (gpre & ~127u) == rtag ? (int)(gpre & 127u) : (1 << 30);
+                    gpre = __hip_atomic_load(gstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                // past the first violating step everything is undone; that step itself is still
+                // checked by every wave (its best violator may be the step's vertex)
+                stop = min(gs, __hip_atomic_load(&s_vmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < t;
+            }
+            unsigned long long lm = KINF;
+            int vlane = -1, vidx = -1;
+            if (wid == 0) {
+                if (stop) {
+                    if (lane == 0) lds_publish(&s_lstop, t);
+                } else {
+                    // the step's pick: the best unattached member ((key, index) order of the select rule)
+                    const unsigned long long lkey = latt ? KINF : mrd_key(lk);
+                    lm = wave_min_u64(lkey);
+                    if (lm < KINF) {
+                        const unsigned long long eqm = __ballot(lkey == lm);
+                        if (__popcll(eqm) == 1) {  // the usual case: one member holds the minimum
+                            vlane = __ffsll((long long)eqm) - 1;
+                        } else {  // equal keys: the largest index
+                            const unsigned long long inv = (lkey == lm) ? (0xffffffffull - (unsigned)li) : ~0ull;
+                            const unsigned long long mi = wave_min_u64(inv);
+                            vlane = last_lane(inv == mi && lkey == lm);
+                        }
+                        vidx = __builtin_amdgcn_readlane(li, vlane);
+                    }
+                    if (lane == 0) {
+                        s_pick[t] = vlane;
+                        s_pkey[t] = lm;
+                        s_pidx[t] = vidx;
+                        lds_publish(&s_tick, t + 1);
+                    }
+                }
+            } else if (!stop) {
+                for (;;) {  // wait for the leader's pick of step t (or its stop)
+                    if (lds_peek(&s_tick) > t) break;
+                    if (lds_peek(&s_lstop) <= t) {
+                        stop = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(0);
+                }
+                if (!stop) {
+                    vlane = s_pick[t];
+                    lm = s_pkey[t];
+                    vidx = s_pidx[t];
+                }
+            }
+            if (tid == 0 || tid == 64) n_exec += (unsigned long long)1 << (tid ? 32 : 0);
+            if (stop) {
+                if (lane == 0) {
+                    s_vt[wid] = 1 << 30;
+                    s_vi[wid] = -1;
+                    s_vk[wid] = KINF;
+                }
+                break;
+            }
+            // does one of this wave's non-members beat the pick?
+            const unsigned long long mk = (att || inl) ? KINF : mrd_key(best);
+            const bool viol = mk < KINF && (mk < lm || (mk == lm && i > vidx));
+            if (__any(viol) || vlane < 0) {
+                const unsigned long long cm = wave_min_u64(mk);
+                const int cl = cm < KINF ? last_lane(mk == cm) : -1;
+                if (lane == 0) {
+                    s_vt[wid] = t;
+                    s_vk[wid] = cm;
+                    atomicMin(&s_vmin, t);
+                    atomicMin(gstop, rtag | (unsigned)t);
+                    if (wid == 0) lds_publish(&s_lstop, t + 1);
+                }
+                if (cl >= 0 && lane == cl) s_vi[wid] = i;
+                if (cl < 0 && lane == 0) s_vi[wid] = -1;
+                break;
+            }
+            // attach the pick and relax against it (own lanes; wave 0 also the list copies)
+            double xv[DM];
+#pragma unroll
+            for (int c = 0; c < DM; c++) xv[c] = s_lrow[vlane][c];
+            const double cv = s_lrow[vlane][DM], ebv = s_lrow[vlane][DM + 1], nnv = s_lrow[vlane][DM + 2];
+            if (wid == 0) {
+                if (lane == vlane) latt = true;
+                if (!latt) {
+                    bool imp = false;
+                    const double mrd = coop_mrd<DM>(in, xv, cv, ebv, nnv, lx, lc, le, ln, lk, imp);
+                    if (imp) lk = mrd;
+                }
+            }
+            if (i == vidx) {
+                att = true;
+                astep = t;
+            }
+            if (!att) {
+                bool imp = false;
+                const double mrd = coop_mrd<DM>(in, xv, cv, ebv, nnv, xi, ci, ebi, nni, best, imp);
+                if (imp) {
+                    b2 = best;
+                    p2 = par;
+                    t2 = tstep;
+                    best = mrd;
+                    par = vidx;
+                    tstep = t;
+                }
+            }
+        }
+        __syncthreads();
+        tick(1);
+        // ---- 3. exchange: first violating step over all waves, the true vertex of that step
+        if (wid == 0) {
+            const int qt = lane < NW ? s_vt[lane] : (1 << 30);
+            int tw = qt;
+            for (int o = 32; o >= 1; o >>= 1) tw = min(tw, __shfl_xor(tw, o));
+            unsigned long long qk = (lane < NW && qt == tw && s_vi[lane] >= 0) ? s_vk[lane] : KINF;
+            const unsigned long long m = wave_min_u64(qk);
+            const int q = m < KINF ? last_lane(qk == m) : -1;  // waves hold increasing indices
+            gu64 *dst = gviol + ((size_t)buf * nwg + bid) * GV;
+            if (lane < GV) {
+                unsigned val;
+                if (lane == 0) val = (unsigned)tw;
+                else if (lane < 3) val = (unsigned)(m >> (32 * (lane - 1)));
+                else val = q >= 0 ? (unsigned)s_vi[q] : 0xffffffffu;
+                put(dst + lane, round, val);
+            }
+            const bool ok = sweep(gviol + (size_t)buf * nwg * GV, nwg * GV, round, s_vg);
+            __builtin_amdgcn_wave_barrier();
+            if (!ok) {
+                if (lane == 0) s_stop = 1;
+            } else {
+                const int gt = lane < nwg ? (int)s_vg[lane * GV] : (1 << 30);
+                int st = gt;
+                for (int o = 32; o >= 1; o >>= 1) st = min(st, __shfl_xor(st, o));
+                const int gi = lane < nwg ? (int)s_vg[lane * GV + 3] : -1;
+                unsigned long long gk = (lane < nwg && gt == st && gi >= 0)
+                                            ? (((unsigned long long)s_vg[lane * GV + 2] << 32) | s_vg[lane * GV + 1])
+                                            : KINF;
+                const unsigned long long gm = wave_min_u64(gk);
+                int wl = -1;
+                if (gm < KINF) {  // largest index among the minima
+                    const unsigned long long inv = (gk == gm) ? (0xffffffffull - (unsigned)gi) : ~0ull;
+                    const unsigned long long mi = wave_min_u64(inv);
+                    wl = last_lane(inv == mi && gk == gm);
+                }
+                if (lane == 0) {
+                    s_star = st;
+                    s_win = wl >= 0 ? (int)s_vg[wl * GV + 3] : -1;
+                    s_stop = 0;
+                }
+                if (wl >= 0) {  // the winner's row from X by index
+                    const int wi = (int)s_vg[wl * GV + 3];
+                    if (lane < DM) s_wrow[lane] = lane < in.d ? in.X[(int64_t)wi * in.d + lane] : 0.0;
+                    else if (lane == DM) s_wrow[DM] = in.core[wi];
+                    else if (lane == DM + 1) s_wrow[DM + 1] = in.eB ? in.eB[wi] : 0.0;
+                    else if (lane == DM + 2) s_wrow[DM + 2] = in.eB ? in.nnB[wi] : 0.0;
+                }
+            }
+        }
+        __syncthreads();
+        if (s_stop) break;
+        tick(2);
+        const int sstar = s_star, win = s_win;
+        // ---- 4. keep steps < s*, undo the rest, attach the true vertex of step s*
+        if (astep != (1 << 30) && astep >= sstar) att = false;  // attached at an undone step
+        // a lane whose last improvement came at an undone step takes back the value before it
+        // (exact when the one before was kept); two or more undone improvements: re-relax
+        const bool undo = !att && tstep >= sstar;
+        const bool redo = undo && t2 >= sstar;
+        if (undo && !redo) {
+            best = b2;
+            par = p2;
+        }
+        if (__any(redo)) {
+            if (redo) {
+                best = best0;
+                par = par0;
+            }
+            for (int u = 0; u < sstar; u++) {
+                const int vl = s_pick[u];
+                double xv[DM];
+#pragma unroll
+                for (int c = 0; c < DM; c++) xv[c] = s_lrow[vl][c];
+                if (redo) {
+                    bool imp = false;
+                    const double mrd = coop_mrd<DM>(in, xv, s_lrow[vl][DM], s_lrow[vl][DM + 1], s_lrow[vl][DM + 2], xi, ci,
+                                                    ebi, nni, best, imp);
+                    if (imp) {
+                        best = mrd;
+                        par = s_lidx[vl];
+                    }
+                }
+            }
+        }
+        committed += sstar;
+        n_spec += sstar;
+        if (win >= 0) {
+            if (i == win) att = true;
+            else if (!att) {
+                double xv[DM];
+#pragma unroll
+                for (int c = 0; c < DM; c++) xv[c] = s_wrow[c];
+                bool imp = false;
+                const double mrd = coop_mrd<DM>(in, xv, s_wrow[DM], s_wrow[DM + 1], s_wrow[DM + 2], xi, ci, ebi, nni, best, imp);
+                if (imp) {
+                    best = mrd;
+                    par = win;
+                }
+            }
+            committed += 1;
+        } else if (sstar == 0) {
+            break;  // nothing left anywhere (cannot happen before n - 1 steps: a safeguard)
+        }
+        n_rounds++;
+        __syncthreads();  // s_pick / s_lrow / s_wrow are rewritten next round
+        tick(3);
+    }
+    if (stats && bid == 0 && tid == 0) {
+        atomicAdd(stats, n_rounds);
+        atomicAdd(stats + 1, n_spec);
+        for (int k = 0; k < 4; k++) atomicAdd(stats + 2 + k, cyc[k]);
+    }
+    if (stats && bid == 0 && (tid == 0 || tid == 64)) atomicAdd(stats + 6, n_exec);  // steps run: wave 0 | wave 1 << 32
+    if (i < n - 1) {
+        va[i] = par >= 0 ? in.ids[par] : 0;
+        vb[i] = in.ids[i];
+        w[i] = best;
+    }
+    if (self_edges && i < n) {
+        va[n - 1 + i] = in.ids[i];
+        vb[n - 1 + i] = in.ids[i];
+        w[n - 1 + i] = in.core[i];
+    }
+}
+
+template <int DM, int BS = 512>  // 512 threads: the registers of two waves per SIMD (1024 spills)
+static bool launch_spec(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
+                        int32_t *va, int32_t *vb, double *w) {
+    const int nwg = (int)ceil_div(n, BS);
+    if (nwg > 64 || n < 2) return false;
+    int coop = 0, ncu = 0, per_cu = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device));
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, prim_spec_kernel<BS, DM>, BS + 64, 0));
+    if (!coop || per_cu < 1 || (int64_t)per_cu * ncu < nwg) return false;
+    constexpr int GC = 3, GV = 4;
+    const int C = std::min(64 / nwg, 2 * (BS / 64));
+    const size_t cbytes = (8 * (size_t)C * GC * 2 * nwg + 255) & ~size_t(255);
+    const size_t vbytes = (8 * (size_t)GV * 2 * nwg + 255) & ~size_t(255);
+    char *base = (char *)arena(ctx, A_WORK3, cbytes + vbytes + 1024);
+    gu64 *gcand = (gu64 *)base;
+    gu64 *gviol = (gu64 *)(base + cbytes);
+    int *err = (int *)(base + cbytes + vbytes);
+    int *xcc = err + 64;
+    unsigned long long *stats = (unsigned long long *)(err + 192);  // rounds, speculated steps
+    unsigned *gstop = (unsigned *)(err + 224);
+    HIP_CHECK(hipMemsetAsync(base, 0, cbytes + vbytes + 1024, ctx->stream));  // tags 0: no round yet
+    HIP_CHECK(hipMemsetAsync(gstop, 0xff, 4, ctx->stream));                   // no violation yet
+    PrimIn L = in;
+    L.X = in.X + o * in.d;
+    L.core = in.core + o;
+    L.ids = in.ids + o;
+    if (in.eB) {
+        L.eB = in.eB + o;
+        L.nnB = in.nnB + o;
+    }
+    int nn = (int)n;
+    int32_t *pva = va + eo, *pvb = vb + eo;
+    double *pw = w + eo;
+    unsigned spin = 1u << 24;
+    int spread1 = 1, res0 = 0;
+    void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &gcand, &gviol, &err, &spin, &spread1, &xcc, &res0, &stats,
+                    &gstop};
+    const int spread = (ctx->prim_coop_xcd && nwg <= ctx->prim_coop_xcd_max_wg && nwg <= 32 * per_cu) ? 8 : 1;
+    static std::atomic<int> launches{0};
+    const int res = spread > 1 ? (launches.fetch_add(1) & 7) : 0;
+    const unsigned plain_spin = 1u << ctx->prim_coop_plain_spin_log2;
+    int h_err = 0;
+    for (int attempt = ctx->prim_coop_plain ? 0 : 1; attempt < 2; attempt++) {
+        if (attempt == 1 && h_err) {
+            HIP_CHECK(hipMemsetAsync(base, 0, cbytes + vbytes + 1024, ctx->stream));
+            HIP_CHECK(hipMemsetAsync(gstop, 0xff, 4, ctx->stream));
+        }
+        {
+            KernelTimer t(ctx, "prim_coop");
+            if (attempt == 0)
+                hipLaunchKernelGGL((prim_spec_kernel<BS, DM>), dim3(nwg * spread), dim3(BS + 64), 0, ctx->stream, L, nn,
+                                   self_edges, pva, pvb, pw, gcand, gviol, err, plain_spin, spread, xcc, res, stats,
+                                   gstop);
+            else
+                HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_spec_kernel<BS, DM>, dim3(nwg), dim3(BS + 64), args, 0,
+                                                     ctx->stream));
+            HIP_CHECK(hipGetLastError());
+        }
+        int64_t *pin = pinned_words(ctx) + PINNED_WORDS - 32;  // private slice: err, rounds, steps
+        HIP_CHECK(hipMemcpyAsync(pin, err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_CHECK(hipMemcpyAsync(pin + 1, stats, 56, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        h_err = (int)(pin[0] & 0xffffffff);
+        if (!h_err) {
+            ctx->stats["prim_coop_steps"] += n - 1;
+            ctx->stats["prim_coop_launches"] += 1;
+            ctx->stats["prim_spec_rounds"] += pin[1];
+            ctx->stats["prim_spec_steps"] += pin[2];
+            static const char *cn[4] = {"prim_spec_cyc_list", "prim_spec_cyc_spec", "prim_spec_cyc_exch", "prim_spec_cyc_commit"};
+            for (int k = 0; k < 4; k++) ctx->stats[cn[k]] += pin[3 + k];
+            ctx->stats["prim_spec_exec_w0"] += pin[7] & 0xffffffff;
+            ctx->stats["prim_spec_exec_w1"] += pin[7] >> 32;
+            return true;
+        }
+        if (attempt == 0) ctx->stats["prim_coop_plain_retries"] += 1;
+    }
+    HDB_THROW(HDB_EDEVICE, "prim_spec: exchange timed out (workgroups not co-resident)");
+    return true;
+}
+
 template <int DM, bool FAST>
 static bool launch_coop2(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
                          int32_t *va, int32_t *vb, double *w) {
@@ -1361,6 +1983,11 @@ void prim_batched_device(hdb_ctx *ctx, const PrimIn &in, const int64_t *h_offs, 
             int64_t n = h_offs[p + 1] - h_offs[p];
             const int64_t o = h_offs[p] - h_offs[0];
             bool ok = false;
+            if (n <= 65536 && ctx->prim_coop_slots == 6) {  // speculative steps, one exchange per round
+                if (in.d <= 4) ok = launch_spec<4>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                else if (in.d <= 8) ok = launch_spec<8>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+                else if (in.d <= 16) ok = launch_spec<16>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
+            }
             if (n <= 65536 && ctx->prim_coop_slots == 4) {  // DPP folds + key/row granules
                 if (in.d <= 4) ok = launch_coop4<4, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
                 else if (in.d <= 8) ok = launch_coop4<8, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);

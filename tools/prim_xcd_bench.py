@@ -14,8 +14,15 @@ pkg = importlib.import_module("232-hierarchical-density-based-clustering-using-m
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 d = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 rng = np.random.default_rng(0)
-X = torch.from_numpy(rng.normal(size=(n, d)) * 10).cuda()
-core = torch.from_numpy(np.abs(rng.normal(0.5, 0.1, n))).cuda()
+if os.environ.get("PRIM_BENCH_DATA", "blobs") == "random":
+    X = torch.from_numpy(rng.normal(size=(n, d)) * 10).cuda()
+    core = torch.from_numpy(np.abs(rng.normal(0.5, 0.1, n))).cuda()
+else:  # blob-shaped rows with k-NN cores (the C5 bubble models' shape)
+    from scipy.spatial import cKDTree
+    C = rng.uniform(-100, 100, (40, d))
+    Xn = C[rng.integers(0, 40, n)] + rng.normal(0, 1, (n, d)) * (1 + 3 * rng.random(n))[:, None]
+    X = torch.from_numpy(Xn).cuda()
+    core = torch.from_numpy(cKDTree(Xn).query(Xn, 4)[0][:, -1].copy()).cuda()
 eB = torch.from_numpy(np.abs(rng.normal(0.3, 0.1, n))).cuda()
 nnB = torch.from_numpy(np.abs(rng.normal(0.2, 0.05, n))).cuda()
 nB = torch.from_numpy(rng.integers(1, 9, n).astype(np.int32)).cuda()
@@ -42,7 +49,14 @@ for rep in range(2):
             if key in out:
                 assert all(np.array_equal(a, b) for a, b in zip(out[key], e)), f"{name}: edges differ with xcd={xcd}"
             out[key] = e
+            try:
+                sr = ctx.get_stat("prim_spec_rounds")
+                spec = f"  spec rounds {sr} steps {ctx.get_stat('prim_spec_steps')} cyc " + " ".join(
+                    str(ctx.get_stat("prim_spec_cyc_" + k)) for k in ("list", "spec", "exch", "commit")) + \
+                    f" exec {ctx.get_stat('prim_spec_exec_w0')} {ctx.get_stat('prim_spec_exec_w1')}"
+            except Exception:
+                spec = ""
             print(f"xcd={xcd} {name:12s} n={n} d={d}: {dt * 1e3:8.2f} ms  ({dt / n * 1e6:.2f} us/step)  "
-                  f"retries {ctx.get_stat('prim_coop_plain_retries') - r0}", flush=True)
+                  f"retries {ctx.get_stat('prim_coop_plain_retries') - r0}{spec}", flush=True)
 ctx.set_option("prim_coop_xcd", 1)
 print("edges identical across xcd settings")
