@@ -163,7 +163,9 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         hipDeviceProp_t prop;
         HIP_CHECK(hipGetDeviceProperties(&prop, device));
         c->num_cus = prop.multiProcessorCount;
-        for (const char *k : {"prim_coop_plain_retries", "prim_coop_steps", "prim_coop_launches", "bubble_knn_replay_overflows"}) c->stats[k] = 0;
+        for (const char *k : {"prim_coop_plain_retries", "prim_coop_steps", "prim_coop_launches", "bubble_knn_replay_overflows",
+                              "boruvka_visits_sum", "boruvka_evals_sum", "boruvka_bound_ns_sum"})
+            c->stats[k] = 0;
         if (const char *e = getenv("HDB_PRIM_COOP_SLOTS")) c->prim_coop_slots = atoi(e);  // A/B knob
         // per-kernel HIP-event timing from birth (contexts created on worker threads, bench.py)
         if (const char *e = getenv("HDB_KERNEL_TIMING")) c->timing = atoi(e) != 0;

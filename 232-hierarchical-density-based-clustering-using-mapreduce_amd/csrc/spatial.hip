@@ -2142,6 +2142,14 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             ctx->stats[r + "_leaves"] = (int64_t)h[1];
             ctx->stats[r + "_nodes"] = (int64_t)h[2];
             tot_evals += (int64_t)h[0];
+            // accumulated over calls (C3/C5 lines: every forced leaf of a job): visits, executed
+            // pair evals and the latency model's lower bound -- one dependent Infinity-Cache round
+            // trip (227 ns) per visit over min(waves, resident wave slots) in flight
+            const int64_t visits = (int64_t)(h[1] + h[2]), waves = (int64_t)h[4];
+            ctx->stats["boruvka_visits_sum"] += visits;
+            ctx->stats["boruvka_evals_sum"] += (int64_t)h[0];
+            if (visits > 0)
+                ctx->stats["boruvka_bound_ns_sum"] += visits * 227 / std::max<int64_t>(1, std::min<int64_t>(waves, 4096));
         }
         hipLaunchKernelGGL(comp_s_kernel, dim3(g), dim3(256), 0, st, pcomp, n, comp_w, best_w, best_s, comp_s);
         hipLaunchKernelGGL(comp_key_kernel, dim3(g), dim3(256), 0, st, pcomp, n, comp_w, comp_s, best_w, best_s,

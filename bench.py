@@ -69,6 +69,20 @@ def cpu_model():
     return "unknown"
 
 
+def thread_cap():
+    """How the CPU-all legs' thread count was set (reported in cpu_baseline: the GPU box exports
+    OMP_NUM_THREADS=16, so the legs run 16 threads there although the affinity mask is larger)."""
+    omp = os.environ.get("OMP_NUM_THREADS")
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    return {"affinity_cpus": aff, "omp_num_threads": int(omp) if omp and omp.isdigit() else None,
+            "threads_used": host_threads(),
+            "cap": (f"OMP_NUM_THREADS={omp} (set by the environment) caps the {aff}-CPU affinity mask"
+                    if omp and omp.isdigit() and int(omp) < aff else f"the whole {aff}-CPU affinity mask")}
+
+
 def host_threads():
     """CPU threads this process may run on (the affinity mask, not the machine's CPU count),
     capped by OMP_NUM_THREADS when set."""
@@ -125,6 +139,7 @@ def cpu_baseline(X, budget_s=10.0):
     tot_1, r_1, m_1 = sample(1, budget_s)
     return {"value": n / tot_all, "unit": "points/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "thread_cap": thread_cap(),
             "sample": f"oracle C -O2, OpenMP {threads} threads: kNN of {r_all} query rows vs all {n} rows "
                       f"(x{n / r_all:.0f}) + reference Prim (parallel scan per step) on a {m_all}-point prefix "
                       f"(x{(n / m_all) ** 2:.0f}); extrapolated full step {tot_all:.0f} s",
@@ -297,6 +312,21 @@ TIMED_KERNELS = ("prim_coop", "prim_block", "prim_step_total", "knn_tree", "boru
 NESTED = {"boruvka_scan"}
 
 
+def boruvka_roofline(scan_s, bound_s, evals, d):
+    """The K2b scan (boruvka_bvh_kernel) on the job's forced leaves above prim_leaf_max: the C2
+    line's latency model -- per round, visits x 227 ns (one dependent Infinity-Cache round trip
+    per node or leaf visit) / min(waves, resident wave slots) -- summed over every round of every
+    leaf in a count_evals pass of the same job (boruvka_bound_ns_sum), over the scan's HIP-event
+    time in the timed jobs; the FP64 fraction of the executed pair evals rides along."""
+    fp64 = 3 * d * evals / scan_s / 1e12 if scan_s > 0 else 0.0
+    return {"bound": "latency", "kernel": "boruvka_bvh_kernel (K2b scan, forced leaves)", "unit": "s",
+            "achieved": scan_s, "peak": bound_s, "frac": bound_s / scan_s if scan_s > 0 else 0.0, "traffic": None,
+            "model": f"per round: visits x {MALL_HIT_NS:.0f} ns / min(waves, {WAVE_SLOTS} resident wave slots), "
+                     "summed over every round of every forced leaf (count_evals pass)",
+            "fp64": {"achieved_tflops": fp64, "peak": FP64_PEAK_TFLOPS, "frac": fp64 / FP64_PEAK_TFLOPS,
+                     "work": "executed pair evals x 3d flops"}}
+
+
 def partitioned_roofline(kt, coop_steps, coop_launches, steps):
     """Latency roofline of the cooperative Prim (prim_coop: the bubble models' and the big
     leaves' reference Prim, the level loop's critical path): every Prim step needs at least
@@ -356,7 +386,7 @@ def partitioned_cpu_baseline(workload, gpu_run=None):
     inst = (f"{cs['n']} x {cs['d']} blobs ({cs['centers']} centres, seed {cs['seed']}), samples/subset "
             f"{cs['samples_per_subset']}, processing_units {cs['processing_units']}, {r['iterations']} levels")
     out = {"value": cs["n"] / dt_all, "unit": "points/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
-           "affinity_cpus": len(os.sched_getaffinity(0)),
+           "affinity_cpus": len(os.sched_getaffinity(0)), "thread_cap": thread_cap(),
            "sample": f"oracle MR-HDBSCAN* loop (mr_driver, C -O2), thread pool of {threads} over each level's "
                      f"subsets and nearest-sample row chunks, on {inst}: {dt_all:.1f} s",
            "single_thread": {"value": cs["n"] / dt_1, "cores": 1, "sample": f"the same instance, 1 thread: {dt_1:.1f} s"}}
@@ -489,6 +519,17 @@ def run_partitioned(args, workload):
     coop_steps = stat_total("prim_coop_steps") - steps0
     coop_launches = stat_total("prim_coop_launches") - launches0
     coop_retries = stat_total("prim_coop_plain_retries") - retries0
+    # diagnostic pass (outside the timed region): per-round visits / waves of every K2b scan
+    for c in list(A.Context._all):
+        c.set_option("count_evals", 1)
+    b0 = {k: stat_total(k) for k in ("boruvka_bound_ns_sum", "boruvka_evals_sum")}
+    job()
+    barrier()
+    for c in list(A.Context._all):
+        c.set_option("count_evals", 0)
+    k2b_roof = boruvka_roofline(kt.get("boruvka_scan", [0.0, 0])[0] / args.steps,
+                                (stat_total("boruvka_bound_ns_sum") - b0["boruvka_bound_ns_sum"]) * 1e-9,
+                                stat_total("boruvka_evals_sum") - b0["boruvka_evals_sum"], cfg["d"])
     if rank == 0:
         w = out["edges"][2].numpy()
         assert w.shape[0] == 2 * n - 1 and np.all(w[:-1] >= w[1:])
@@ -518,6 +559,13 @@ def run_partitioned(args, workload):
                 "predicted_scaling": predicted_scaling(drv, importlib.import_module(PKG + ".parallel"))
                 if args.phases and world == 1 else None,
                 "roofline": partitioned_roofline(kt, coop_steps, coop_launches, args.steps)}
+        line["roofline"]["boruvka"] = k2b_roof
+        dom = line["roofline"]["dominant_kernel"]
+        if dom in ("boruvka_total", "boruvka_scan", "exact_leaf_total") and k2b_roof["achieved"] > 0:
+            # the dominant kernel is K2b: the line's top-level roofline is K2b's, the Prim's rides along
+            prim_roof = {k: v for k, v in line["roofline"].items() if k != "boruvka"}
+            line["roofline"] = dict(k2b_roof) | {"dominant_kernel": dom, "dominant_kernel_s": prim_roof["dominant_kernel_s"],
+                                                 "prim_coop": prim_roof}
         if world == 1 and not args.no_cpu_baseline:
             def gpu_run(Xs, cs):
                 d2 = pkg.MRHDBSCANStar(minPts=MIN_PTS, minClSize=MIN_CL_SIZE, processing_units=cs["processing_units"],
