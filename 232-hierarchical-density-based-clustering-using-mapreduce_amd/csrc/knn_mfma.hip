@@ -385,6 +385,16 @@ constexpr int NW = HDB_K1S_WAVES;
 #ifndef HDB_K1S_PROF
 #define HDB_K1S_PROF 0  // diagnostic build: per-wave cycle split of the screen loop (stats k1s_prof_*)
 #endif
+// (round 5 measured two ways of writing the screen's log entries in larger pieces -- an
+// 8-entry LDS buffer per (query, half) flushed 64 bytes at a time, and entry pairs held in
+// registers and stored as 16 bytes: HBM writes 6.54 -> 3.04 / 5.09 GB per launch at C4, but
+// the screen took 36.9 -> 38.2 / 39.0 ms, the longer hit path costing more than the traffic)
+#ifndef HDB_K1S_HACC
+#define HDB_K1S_HACC 1  // REG hit path: the hit's screen value from an LDS copy of the lane's 16 (see hacc_s)
+#endif
+#ifndef HDB_K1F_XCD
+#define HDB_K1F_XCD 1  // K1m re-check: contiguous 16-query workgroup ranges per XCD (shared candidate rows in one L2)
+#endif
 #define K1S_XCD HDB_K1S_XCD
 // Workgroups are dealt round-robin over the 8 XCDs (block b runs on XCD b mod 8); this maps
 // them so XCD x takes one contiguous range of logical blocks (a bijection on [0, G)).
@@ -406,16 +416,50 @@ struct ScreenCfg {
     static constexpr int BUF = 2 * 32 * DP;       // bf16 elements per staged block (hi rows, lo rows)
 };
 
-__device__ __forceinline__ float f32_down(double x) {
-    float f = (float)x;
-    if ((double)f > x) f = nextafterf(f, -INFINITY);
-    return f;
+// Cross-lane steps without LDS round trips (ds_bpermute: one LDS trip per step, and a chain of
+// them per reduction): DPP inside a 16-lane row, v_permlane{16,32}_swap (gfx950) across rows.
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HMIRROR = 0x141, DPP_MIRROR = 0x140;
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    const int b = __float_as_int(v);  // (a lane whose source is off keeps its own value)
+    return __int_as_float(__builtin_amdgcn_update_dpp(b, b, CTRL, 0xf, 0xf, false));
 }
-__device__ __forceinline__ float f32_up(double x) {
-    float f = (float)x;
-    if ((double)f < x) f = nextafterf(f, INFINITY);
-    return f;
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)b, (int)b, CTRL, 0xf, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+// the value of lane ^ 32: v_permlane32_swap(v, v) leaves the low half's values in the first
+// result's high half and the high half's values in the second result's low half
+__device__ __forceinline__ float xor32_f(float v, int lane) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(lane < 32 ? p[1] : p[0]);
+}
+// maximum over the wave, in every lane (a row's own and partner values both sit in the swap's
+// two results, so the symmetric max needs no lane select)
+__device__ __forceinline__ float wave_max_f(float v) {
+    v = fmaxf(v, dpp_f<DPP_XOR1>(v));
+    v = fmaxf(v, dpp_f<DPP_XOR2>(v));
+    v = fmaxf(v, dpp_f<DPP_HMIRROR>(v));
+    v = fmaxf(v, dpp_f<DPP_MIRROR>(v));
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(v, fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1])));
+    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(v, fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1])));
+}
+// minimum over each 16-lane row, in every lane of the row
+__device__ __forceinline__ double row_min_d(double v) {
+    v = fmin(v, dpp_d<DPP_XOR1>(v));
+    v = fmin(v, dpp_d<DPP_XOR2>(v));
+    v = fmin(v, dpp_d<DPP_HMIRROR>(v));
+    return fmin(v, dpp_d<DPP_MIRROR>(v));
+}
+
+// directed conversions (largest float <= x, smallest float >= x), branch-free
+__device__ __forceinline__ float f32_down(double x) { return __double2float_rd(x); }
+__device__ __forceinline__ float f32_up(double x) { return __double2float_ru(x); }
 
 // per-block screen constants, packed so one global_load_lds stages them
 __global__ void screen_consts_kernel(const double *__restrict__ nrm2, const double *__restrict__ nrm, int64_t n_pad,
@@ -426,7 +470,8 @@ __global__ void screen_consts_kernel(const double *__restrict__ nrm2, const doub
         // a padding row of the layout never passes the screen (hc = +inf)
         b[i] = perm[r] < 0 ? INFINITY : (float)(nrm2[r] * (1.0 - 4e-6) * 0.5);
         b[32 + i] = (float)nrm[r];
-        ((double *)(b + 64))[i] = nrm2[r];
+        // |c|^2 of a padding row is NaN: its exact-test bound lb = NaN never passes lb <= thr
+        ((double *)(b + 64))[i] = perm[r] < 0 ? __builtin_nan("") : nrm2[r];
         ((double *)(b + 128))[i] = nrm[r];
     }
 }
@@ -798,6 +843,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     __shared__ unsigned short si_s[NSB_MAX];  // superblock ids in key order, then their block counts
     __shared__ int sbs_s[NSB_MAX];            // first block of the i-th superblock in key order
     __shared__ float tmax_s[2][NW];           // per-wave max thr, written in alternate iterations
+    // REG hit path: a hitting lane's 16 screen values, read back by (dynamic) row index -- an
+    // LDS load in place of a 16-way register select chain per hit
+    __shared__ __attribute__((aligned(16))) float hacc_s[REG && HDB_K1S_HACC ? NW * 64 * 16 : 1];
 
     // the wave index as a scalar: the LDS-DMA destinations (M0) and buffer resources derived
     // from it stay in SGPRs (no waterfall loop, no VGPRs spent on uniform addresses)
@@ -913,7 +961,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     auto union_kth = [&]() __attribute__((always_inline)) {
         float pv[KR];
 #pragma unroll
-        for (int k = 0; k < KR; k++) pv[k] = __shfl_xor(tl[k], 32);
+        for (int k = 0; k < KR; k++) pv[k] = xor32_f(tl[k], lane);
         float th = fminf(pv[KT], tl[KT]);
 #pragma unroll
         for (int i = 1; i < KR; i++) th = fminf(th, fmaxf(tl[i - 1], pv[KT - i]));
@@ -1074,15 +1122,20 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
                 int hh = half;
                 asm volatile("" : "+v"(hh));  // as cq: the half-log base is not hoisted (a 64-bit spill)
                 LogEnt *const L = logs + (qid * S_LOGCAP + hh * LH);
+                float *const hv = hacc_s + (HDB_K1S_HACC ? (wave * 64 + lane) * 16 : 0);
+                if (HDB_K1S_HACC)
+#pragma unroll
+                    for (int u = 0; u < 16; u += 4)
+                        *(float4 *)(hv + u) = make_float4(acc[0][u], acc[0][u + 1], acc[0][u + 2], acc[0][u + 3]);
                 for (; mk; mk &= mk - 1) {
                     const int r = __builtin_ctz(mk);
                     const int ci = 8 * (r >> 2) + 4 * half + (r & 3);
 #if HDB_K1S_PROF
                     p_hits++;
 #endif
-                    const float av = acc[0][r];  // dynamic element
+                    const float av = HDB_K1S_HACC ? hv[r] : acc[0][r];  // dynamic element
                     const int64_t cid = cb + ci;
-                    if ((ex && cid == qid) || cst_s[ci] == INFINITY) continue;  // self / padding row
+                    if (ex && cid == qid) continue;  // self (a padding row fails the lb test: c2 = NaN)
                     const double c2 = c2d[ci], cn = cnd[ci];
                     const double approx = (q2 + c2) - 2.0 * (double)av;
                     const double bound = eps_dot * qn * cn + 4e-13 * (q2 + c2) + 1e-30;
@@ -1113,8 +1166,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
             thq = union_kth();
             const float th = thq;
             a[0] = qh[0] - 0.5f * th;
-            float wm = (qvm & 1u) ? th : -INFINITY;
-            for (int o = 32; o >= 1; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o));
+            const float wm = wave_max_f((qvm & 1u) ? th : -INFINITY);
             wmax = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wm)));  // uniform
 #if HDB_K1S_PROF
             p_hit += __builtin_readcyclecounter() - p_c;
@@ -1157,10 +1209,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
 #endif
                             const float av = acc[t][r];  // dynamic element (rare path)
                             const int64_t cid = cb + ci;
-                            // padding rows carry hc = +inf in the staged constants (an LDS read:
-                            // no dependent global load -- its vmcnt wait would also drain the
-                            // next block's LDS-DMA prefetch)
-                            if ((ex && cid == qid) || cst_s[ci] == INFINITY) continue;
+                            if (ex && cid == qid) continue;  // self (a padding row fails the lb test: c2 = NaN)
                             const double c2 = c2d[ci], cn = cnd[ci];
                             const double approx = (q2 + c2) - 2.0 * (double)av;
                             const double bound = eps_dot * qn * cn + 4e-13 * (q2 + c2) + 1e-30;
@@ -1358,7 +1407,9 @@ __global__ __launch_bounds__(256, HDB_K1F_WPE) void knn_mfma_final16_kernel(cons
     __shared__ int cl_s[16][K1F_CH];
     const int lane = threadIdx.x & 63, sub = lane >> 4, sl = lane & 15;
     const int g = (threadIdx.x >> 6) * 4 + sub;  // query slot in the workgroup
-    const int64_t q = (int64_t)blockIdx.x * 16 + g;
+    // consecutive workgroups (one k-means cluster) share candidate rows: with XCD-contiguous
+    // ranges those rows are fetched into one L2 instead of eight
+    const int64_t q = (HDB_K1F_XCD ? xcd_contig(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x) * 16 + g;
     const bool act = q < n && perm[q] >= 0;  // n: layout rows here (uniform per 16 lanes)
     const int rs = LAY ? DP : d;  // query row length in LDS
     double *qr = k1f_dyn + (size_t)g * rs;
@@ -1423,9 +1474,7 @@ __global__ __launch_bounds__(256, HDB_K1F_WPE) void knn_mfma_final16_kernel(cons
 #pragma unroll 1
                     for (int k = 0; k < KC; k++) {
                         const double m = fmin(fmin(lv, fmin(v[0], v[1])), fmin(v[2], v[3]));
-                        double mn = m;
-#pragma unroll
-                        for (int o = 8; o >= 1; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
+                        const double mn = row_min_d(m);
                         const unsigned long long b = (__ballot(m == mn) >> (16 * sub)) & 0xFFFFull;
                         if (sl == __ffsll((long long)b) - 1) {  // the first lane holding it gives it up
                             if (lv == mn) lv = INFINITY;
