@@ -182,6 +182,8 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         if (const char *e = getenv("HDB_FLAT_DEEP")) c->flat_deep_depth = atoi(e);          // A/B knob
         if (const char *e = getenv("HDB_FLAT_DEEP_ROOT")) c->flat_deep_root = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_FLAT_DEEP_LINK")) c->flat_deep_link = atoi(e);      // A/B knob
+        if (const char *e = getenv("HDB_BOR_EARLY_PTS")) c->boruvka_early_pts = atoi(e);    // A/B knob
+        if (const char *e = getenv("HDB_BOR_EARLY_ROUNDS")) c->boruvka_early_rounds = atoi(e);  // A/B knob
         *out = c;
         return HDB_OK;
     } catch (const Error &e) {

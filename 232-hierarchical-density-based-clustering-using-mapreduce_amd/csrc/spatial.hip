@@ -1333,6 +1333,12 @@ __global__ void self_keys_kernel(const double *__restrict__ core, int64_t n, dou
         id[i] = (int32_t)i;
     }
 }
+// the sorted self edges' weights: the cores themselves (a -0.0 core stays -0.0, as the plain
+// path writes it; the sort keys normalised it to +0.0, which the merge's comparisons tie anyway)
+__global__ void gather_core_kernel(const double *__restrict__ core, const int32_t *__restrict__ perm, int64_t n,
+                                   double *__restrict__ w) {
+    HDB_GRID_STRIDE(i, n) w[i] = core[perm[i]];
+}
 __global__ void edge_out_kernel(const int32_t *perm_, const int32_t *a, const int32_t *b, const double *ww, int64_t m,
                                 int32_t *oa, int32_t *ob, double *ow) {
     HDB_GRID_STRIDE(i, m) {
@@ -2239,6 +2245,7 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
                     HIP_CHECK(sort_pairs_desc(nullptr, tb2, sk, sk2, si, sperm, n, 0, 64, st));
                     void *tmp2 = arena(ctx, A_SORT, tb2);
                     HIP_CHECK(sort_pairs_desc(tmp2, tb2, sk, sk2, si, sperm, n, 0, 64, st));
+                    hipLaunchKernelGGL(gather_core_kernel, dim3(g), dim3(256), 0, st, self_core, sperm, n, sk2);
                     merge_two_runs_device(ctx, ta, tbv, tw, ne, sperm, sperm, sk2, n, va, vb, w);
                 }
             }

@@ -153,10 +153,10 @@ MFMA_BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
 # HBM bytes per launch from the PMC passes of this build (FETCH_SIZE / WRITE_SIZE runs of their
 # own, corrected by tools/pmc_summary.py): tools/profile_bench.sh (C2), tools/profile_c4.sh (C4)
 PMC_C2 = next((p for p in (os.path.join(ROOT, "profiles", r, "final", "prof_c2", "pmc_summary.json")
-                            for r in ("r04", "r03", "r02")) if os.path.exists(p)),
+                            for r in ("r05", "r04", "r03", "r02")) if os.path.exists(p)),
               os.path.join(ROOT, "profiles", "r02", "final", "prof_c2", "pmc_summary.json"))
 PMC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, "c4_final", "pmc_summary.json")
-                            for r in ("r04", "r03", "r02")) if os.path.exists(p)),
+                            for r in ("r05", "r04", "r03", "r02")) if os.path.exists(p)),
               os.path.join(ROOT, "profiles", "r02", "c4_final", "pmc_summary.json"))
 
 
@@ -293,7 +293,7 @@ def run_c4(args):
                                 "sample": f"oracle C -O2, OpenMP {threads} threads: core distances of {rows.shape[0]} "
                                           f"query rows vs all {n} rows (x{n / rows.shape[0]:.0f}); "
                                           f"extrapolated full step {full:.0f} s"}
-    print(json.dumps(line), flush=True)
+    emit(line)
 
 
 PARTITIONED = {  # SURVEY.md §8(d) C3 / C5 (recursive sampling, data bubbles), strong scaling
@@ -584,9 +584,23 @@ def run_partitioned(args, workload):
                         best = dt2 if best is None else min(best, dt2)
                 return best
             line["cpu_baseline"] = partitioned_cpu_baseline(workload, gpu_run)
-        print(json.dumps(line), flush=True)
+        emit(line)
     if world > 1:
         dist.destroy_process_group()
+
+
+# Definitions of the line's keys changed in round 4: `value` includes the
+# pinned-host H2D (round 3: HBM-resident inputs), the HBM-resident rate is `hbm_resident_*`
+# (round 3's `pcie_inclusive_*` meant the opposite), and C4's `mrd_evals_per_s` counts executed
+# screen pairs (the all-pairs-equivalent rate is `all_pairs_equivalent_evals_per_s`).
+LINE_SCHEMA = 4
+LINE_SCHEMA_NOTE = ("v4 (since round 4): value includes the pinned-host H2D; hbm_resident_* = HBM-resident "
+                    "inputs (r03's pcie_inclusive_* meant the opposite); C4 mrd_evals_per_s = executed screen pairs")
+
+
+def emit(line):
+    line = dict(line, schema=LINE_SCHEMA, schema_note=LINE_SCHEMA_NOTE)
+    print(json.dumps(line), flush=True)
 
 
 def main():
@@ -1058,7 +1072,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(X_host)
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        emit(line)
     if world > 1:
         dist.destroy_process_group()
 
