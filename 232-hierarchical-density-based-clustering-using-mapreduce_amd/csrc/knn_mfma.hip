@@ -376,12 +376,6 @@ constexpr int NW = HDB_K1S_WAVES;
 // holds bounds of distinct candidates: >= the KC-th exact value), refreshed per hit step
 #define HDB_K1S_REGTOP 1
 #endif
-#ifndef HDB_KM_MFMA
-#define HDB_KM_MFMA 1  // k-means assignment of the layout on the matrix cores (km_assign_mfma_kernel)
-#endif
-#ifndef HDB_K1S_SBKEYS
-#define HDB_K1S_SBKEYS 1  // superblock visiting keys of all groups in one grid up front (sb_keys_kernel)
-#endif
 #ifndef HDB_K1S_PROF
 #define HDB_K1S_PROF 0  // diagnostic build: per-wave cycle split of the screen loop (stats k1s_prof_*)
 #endif
@@ -389,9 +383,6 @@ constexpr int NW = HDB_K1S_WAVES;
 // 8-entry LDS buffer per (query, half) flushed 64 bytes at a time, and entry pairs held in
 // registers and stored as 16 bytes: HBM writes 6.54 -> 3.04 / 5.09 GB per launch at C4, but
 // the screen took 36.9 -> 38.2 / 39.0 ms, the longer hit path costing more than the traffic)
-#ifndef HDB_K1S_HACC
-#define HDB_K1S_HACC 1  // REG hit path: the hit's screen value from an LDS copy of the lane's 16 (see hacc_s)
-#endif
 #ifndef HDB_K1F_XCD
 #define HDB_K1F_XCD 1  // K1m re-check: contiguous 16-query workgroup ranges per XCD (shared candidate rows in one L2)
 #endif
@@ -539,43 +530,6 @@ __global__ void km_init_kernel(const float *__restrict__ Y, int64_t n, float *__
     const int c = blockIdx.x, p = threadIdx.x;
     const int64_t r = (int64_t)(((unsigned long long)hash_u32(c * 2654435761u + 17u) * (unsigned long long)n) >> 32);
     C[c * KM_P + p] = Y[r * KM_P + p];
-}
-
-// nearest centroid of every row (centroids staged in LDS); sums by global atomics
-__global__ __launch_bounds__(512) void km_assign_kernel(const float *__restrict__ Y, int64_t n, int64_t step, int k,
-                                                        const float *__restrict__ C, int *__restrict__ asg,
-                                                        float *__restrict__ sum, float *__restrict__ cnt,
-                                                        int *__restrict__ hist) {
-    __shared__ float c_s[KM_K * KM_P];
-    for (int i = threadIdx.x; i < k * KM_P; i += blockDim.x) c_s[i] = C[i];
-    __syncthreads();
-    HDB_GRID_STRIDE(ii, n) {
-        const int64_t i = ii * step;  // the Lloyd iterations run on a strided sample
-        float y[KM_P];
-#pragma unroll
-        for (int p = 0; p < KM_P; p++) y[p] = Y[i * KM_P + p];
-        float best = INFINITY;
-        int bc = 0;
-        for (int c = 0; c < k; c++) {
-            float s2 = 0.f;
-#pragma unroll
-            for (int p = 0; p < KM_P; p++) {
-                const float e = y[p] - c_s[c * KM_P + p];
-                s2 = fmaf(e, e, s2);
-            }
-            if (s2 < best) {
-                best = s2;
-                bc = c;
-            }
-        }
-        asg[i] = bc;
-        if (hist) atomicAdd(&hist[bc], 1);
-        if (sum) {
-#pragma unroll
-            for (int p = 0; p < KM_P; p++) atomicAdd(&sum[bc * KM_P + p], y[p]);
-            atomicAdd(&cnt[bc], 1.f);
-        }
-    }
 }
 
 // The same assignment on the matrix cores: argmin_c |c|^2 - 2 y.c with y and c rounded to
@@ -751,7 +705,7 @@ struct SbArgs {
     int nsb;                   // superblocks (<= NSB_MAX)
     int prune;                 // 0: every superblock in index order
     unsigned long long *blocks_done;
-    const float *keys;         // [groups][nsbp] visiting keys from sb_keys_kernel (null: in the screen)
+    const float *keys;         // [groups][nsbp] visiting keys from sb_keys_kernel
 };
 
 // The superblock visiting keys of every (query group, superblock) pair, computed up front in
@@ -845,7 +799,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     __shared__ float tmax_s[2][NW];           // per-wave max thr, written in alternate iterations
     // REG hit path: a hitting lane's 16 screen values, read back by (dynamic) row index -- an
     // LDS load in place of a 16-way register select chain per hit
-    __shared__ __attribute__((aligned(16))) float hacc_s[REG && HDB_K1S_HACC ? NW * 64 * 16 : 1];
+    __shared__ __attribute__((aligned(16))) float hacc_s[REG ? NW * 64 * 16 : 1];
 
     // the wave index as a scalar: the LDS-DMA destinations (M0) and buffer resources derived
     // from it stay in SGPRs (no waterfall loop, no VGPRs spent on uniform addresses)
@@ -890,32 +844,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
     int nsbp = 1;
     while (nsbp < sb.nsb) nsbp <<= 1;
     if (sb.prune) {
-        if (sb.keys) {  // precomputed (sb_keys_kernel): one coalesced row
-            for (int i = tid; i < nsbp; i += 64 * NW) {
-                sk_s[i] = sb.keys[gid * nsbp + i];
-                si_s[i] = (unsigned short)i;
-            }
-        } else {
-        const double *mq = sb.qctr + gid * DP;
-        const double RQ = sb.qrn[2 * gid], NQ = sb.qrn[2 * gid + 1];
+        // keys precomputed by sb_keys_kernel: one coalesced row
         for (int i = tid; i < nsbp; i += 64 * NW) {
-            float key = INFINITY;
-            if (i < sb.nsb) {
-                const double *ms = sb.sctr + (int64_t)i * DP;
-                double d2 = 0.0;
-                for (int c = 0; c < DP; c++) {
-                    const double e = mq[c] - ms[c];
-                    d2 += e * e;
-                }
-                const double RS = sb.srn[2 * i], NS = sb.srn[2 * i + 1];
-                const double gap = sqrt(d2) * (1.0 - 1e-12) - (RQ + RS) * (1.0 + 1e-12);
-                const double lb2 = gap > 0.0 ? gap * gap * (1.0 - 1e-12) : 0.0;
-                const double bm = eps_dot * NQ * NS + 4e-13 * (NQ * NQ + NS * NS) + 1e-30;
-                key = f32_down(lb2 - 2.0 * bm * (1.0 + 1e-12));
-            }
-            sk_s[i] = key;
+            sk_s[i] = sb.keys[gid * nsbp + i];
             si_s[i] = (unsigned short)i;
-        }
         }
         __syncthreads();
         for (int k = 2; k <= nsbp; k <<= 1)
@@ -1122,18 +1054,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
                 int hh = half;
                 asm volatile("" : "+v"(hh));  // as cq: the half-log base is not hoisted (a 64-bit spill)
                 LogEnt *const L = logs + (qid * S_LOGCAP + hh * LH);
-                float *const hv = hacc_s + (HDB_K1S_HACC ? (wave * 64 + lane) * 16 : 0);
-                if (HDB_K1S_HACC)
+                float *const hv = hacc_s + (wave * 64 + lane) * 16;
 #pragma unroll
-                    for (int u = 0; u < 16; u += 4)
-                        *(float4 *)(hv + u) = make_float4(acc[0][u], acc[0][u + 1], acc[0][u + 2], acc[0][u + 3]);
+                for (int u = 0; u < 16; u += 4)
+                    *(float4 *)(hv + u) = make_float4(acc[0][u], acc[0][u + 1], acc[0][u + 2], acc[0][u + 3]);
                 for (; mk; mk &= mk - 1) {
                     const int r = __builtin_ctz(mk);
                     const int ci = 8 * (r >> 2) + 4 * half + (r & 3);
 #if HDB_K1S_PROF
                     p_hits++;
 #endif
-                    const float av = HDB_K1S_HACC ? hv[r] : acc[0][r];  // dynamic element
+                    const float av = hv[r];  // dynamic element (LDS: no 16-way register select chain)
                     const int64_t cid = cb + ci;
                     if (ex && cid == qid) continue;  // self (a padding row fails the lb test: c2 = NaN)
                     const double c2 = c2d[ci], cn = cnd[ci];
@@ -1593,24 +1524,14 @@ static int64_t km_layout(hdb_ctx *ctx, const __bf16 *Xh, int DP, int d, int64_t 
     HIP_CHECK(hipMemsetAsync(b.hist, 0, 4 * (size_t)KM_K, st));
     // Lloyd iterations on a strided sample of <= 128k rows, then every row once
     const int64_t step = std::max<int64_t>(1, n / 131072), m = n / step;
-    const int gs = (int)std::min<int64_t>(ceil_div(m, 512), 1024);
     for (int it = 0; it < KM_IT; it++) {
-        if (HDB_KM_MFMA)
-            hipLaunchKernelGGL(km_assign_mfma_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(m, 32 * KMA_WAVES), 2048)),
-                               dim3(64 * KMA_WAVES), 0, st, b.Y, m, step, k, b.C, b.asg, b.sum, b.cnt, (int *)nullptr);
-        else
-            hipLaunchKernelGGL(km_assign_kernel, dim3(gs), dim3(512), 0, st, b.Y, m, step, k, b.C, b.asg, b.sum,
-                               b.cnt, (int *)nullptr);
+        hipLaunchKernelGGL(km_assign_mfma_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(m, 32 * KMA_WAVES), 2048)),
+                           dim3(64 * KMA_WAVES), 0, st, b.Y, m, step, k, b.C, b.asg, b.sum, b.cnt, (int *)nullptr);
         hipLaunchKernelGGL(km_update_kernel, dim3(k), dim3(KM_P), 0, st, b.C, b.sum, b.cnt);
     }
-    const int ga = (int)std::min<int64_t>(ceil_div(n, 512), 1024);
-    if (HDB_KM_MFMA)
-        hipLaunchKernelGGL(km_assign_mfma_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 32 * KMA_WAVES), 2048)),
-                           dim3(64 * KMA_WAVES), 0, st, b.Y, n, (int64_t)1, k, b.C, b.asg, (float *)nullptr,
-                           (float *)nullptr, b.hist);
-    else
-        hipLaunchKernelGGL(km_assign_kernel, dim3(ga), dim3(512), 0, st, b.Y, n, (int64_t)1, k, b.C, b.asg,
-                           (float *)nullptr, (float *)nullptr, b.hist);
+    hipLaunchKernelGGL(km_assign_mfma_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 32 * KMA_WAVES), 2048)),
+                       dim3(64 * KMA_WAVES), 0, st, b.Y, n, (int64_t)1, k, b.C, b.asg, (float *)nullptr,
+                       (float *)nullptr, b.hist);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(km_keys_kernel, dim3(g), dim3(256), 0, st, b.Y, b.asg, n, b.k1, b.vals);
     size_t tb = b.tmp_bytes;
@@ -1786,7 +1707,7 @@ static bool knn_mfma_dp(hdb_ctx *ctx, const double *X, int64_t n, int d, int KC,
         unsigned long long *blocks_done = stats + 1;
         HIP_CHECK(hipMemsetAsync(blocks_done, 0, HDB_K1S_PROF ? 64 : 8, st));
         float *sb_keys = nullptr;
-        if (prune && HDB_K1S_SBKEYS) {
+        if (prune) {
             int nsbp = 1;
             while (nsbp < nsb) nsbp <<= 1;
             const int64_t ngr = n_lp / Cf::SQ;

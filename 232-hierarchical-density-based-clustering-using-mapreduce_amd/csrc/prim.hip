@@ -878,9 +878,6 @@ static bool launch_coop3(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
 // line stays in that XCD's L2, which every CU's sc1 poll reads) instead of sc1 stores (which
 // drop the line from L2, so every poll crossed the fabric).  Any other placement keeps the sc1
 // protocol: placement changes only speed.
-#ifndef HDB_COOP_CACHE
-#define HDB_COOP_CACHE 1
-#endif
 template <int BS, int DM, bool FULL>
 __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int self_edges, int32_t *__restrict__ va,
                                                         int32_t *__restrict__ vb, double *__restrict__ w,
@@ -962,7 +959,7 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
     }
     int cur = n - 1;
     constexpr unsigned long long KINF = 0x7ff0000000000000ull;  // key of +inf: nothing to offer
-    // Candidate caching (HDB_COOP_CACHE): a wave's candidate changes only when one of its lanes
+    // Candidate caching: a wave's candidate changes only when one of its lanes
     // improved or its parked winner was attached in the last step, and a workgroup's only when
     // one of its waves' did -- most steps relax nothing near most waves (the sqrt-free rejection
     // in coop_mrd), so the wave minimum, the parking and the workgroup fold are skipped and the
@@ -981,7 +978,7 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
             par = cur;
         }
         COOP_T(6);
-        const bool dirty = !HDB_COOP_CACHE || step == 1 || __any(imp || just);
+        const bool dirty = step == 1 || __any(imp || just);
         just = false;
         if (dirty) {
             const unsigned long long key = att ? KINF : mrd_key(best);
@@ -1005,7 +1002,7 @@ __global__ __launch_bounds__(BS) void prim_coop4_kernel(PrimIn in, int n, int se
             const int buf = step & 1;
             const unsigned tag = (unsigned)step;
             unsigned val;
-            if (!HDB_COOP_CACHE || s_dirty) {
+            if (s_dirty) {
                 // fold the waves: lane q holds wave q's candidate
                 const int qi = lane < NW ? s_ci[lane] : -1;
                 const unsigned long long qk = qi >= 0 ? mrd_key(s_cand[lane < NW ? lane : 0][ND]) : KINF;

@@ -490,9 +490,8 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
 #ifndef HDB_BOR_REFRESH_LOG2
 #define HDB_BOR_REFRESH_LOG2 3  // K2b: re-read the component bound every 2^x node visits
 #endif
-#ifndef HDB_BOR_LEAF_PUBLISH
-#define HDB_BOR_LEAF_PUBLISH 2  // K2b: publish a better edge to the component bound at once -- 1: per lane (round 3; its same-address atomics cost more than the pruning buys), 0: never (the wave tail still publishes), 2: one DPP minimum and at most one atomic per wave (A/B r04: scan 4.35 (1) -> 3.90 (0); 3.22 (0) -> 2.84 ms (2))
-#endif
+// K2b leaf publish: a better edge reaches the component bound at once, one DPP minimum and at
+// most one atomic per wave (A/B r04: per-lane atomics 4.35 ms, never 3.90, per wave 2.84 ms)
 #ifndef HDB_BOR_ROWS
 #define HDB_BOR_ROWS 1  // K2b leaf groups needed by few lanes: (query, candidate) pairs in 16-lane rows
 #endif
@@ -565,9 +564,6 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
     const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
-#ifndef HDB_TRAV_DPP
-#define HDB_TRAV_DPP 1  // K1t/K2b traversal: DPP subgroup maxima and readlane ranking instead of __shfl
-#endif
 
 // Pushes the children of internal node (lev, idx) that some lane needs, farthest first
 // (so the nearest is popped first), ordered by box-to-box distance from the query box.
@@ -608,7 +604,7 @@ __device__ __forceinline__ void push_children(const Bvh &bvh, const int64_t *off
     int rank = 0;
 #pragma unroll
     for (int j = 0; j < FAN; j++) {
-        const double kj = HDB_TRAV_DPP ? readlane_f64(key, j) : __shfl(key, j);
+        const double kj = readlane_f64(key, j);  // (DPP/readlane, no LDS trips)
         const bool okj = (okmask >> j) & 1u;
         rank += (okj && (kj > key || (kj == key && j < lane))) ? 1 : 0;
     }
@@ -618,9 +614,7 @@ __device__ __forceinline__ void push_children(const Bvh &bvh, const int64_t *off
     sp += __popc(okmask);
 }
 
-#ifndef HDB_BOR_SUBTEST
-#define HDB_BOR_SUBTEST 1  // K2b child / group tests lane-parallel against 8-lane subgroup boxes
-#endif
+// K2b child / group tests lane-parallel against 8-lane subgroup boxes (push_children_sub)
 // The same push with a lane-parallel pre-filter: lane L tests child L & 7 against the box of
 // its 8-lane subgroup L >> 3 (ok(a, b, tag): a superset of what the subgroup's lanes need),
 // then only the children that pass are tested per lane (needs) -- the same children as
@@ -678,7 +672,7 @@ __device__ __forceinline__ void push_children_sub(const Bvh &bvh, const int64_t 
     int rank = 0;
 #pragma unroll
     for (int j = 0; j < FAN; j++) {
-        const double kj = HDB_TRAV_DPP ? readlane_f64(key, j) : __shfl(key, j);
+        const double kj = readlane_f64(key, j);  // (DPP/readlane, no LDS trips)
         const bool okj = (okmask >> j) & 1u;
         rank += (okj && (kj > key || (kj == key && j < lane))) ? 1 : 0;
     }
@@ -731,9 +725,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
     __shared__ int32_t boxt_s[4][FAN];
     __shared__ int64_t lvl_s[4][2 * (MAXLEV + 1)];
     __shared__ double q_s[4][2 * D];
-#if HDB_BOR_SUBTEST
     __shared__ double sg_s[4][8 * 2 * D];
-#endif
 #if HDB_BOR_ROWS
     // row-batched leaf groups: the wave's query points (staged once) and per group the needing
     // lanes' bounds and the passing pairs' keys
@@ -837,7 +829,6 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
         }
     }
     __builtin_amdgcn_wave_barrier();
-#if HDB_BOR_SUBTEST
     // 8-lane subgroups (consecutive work entries: Morton-close points).  Every node and group
     // test below runs once per (child, subgroup) pair on its own lane, with the box of the
     // subgroup's points, the largest bound among its searching lanes and the component they
@@ -874,10 +865,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
     // the subgroup's largest bound over its lanes still searching (-1: none)
     auto sub_bound = [&]() -> double {
         double m = (search & !(mlb > cwv)) ? bound() : -1.0;
-        if (HDB_TRAV_DPP) return sub8_max(m);
-#pragma unroll
-        for (int off = 1; off < 8; off <<= 1) m = fmax(m, __shfl_xor(m, off));
-        return m;
+        return sub8_max(m);
     };
     auto sub_ok = [&](double mb) {
         return [&, mb](const double (&a)[D], const double (&b)[D], int32_t tg) -> bool {
@@ -906,7 +894,6 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
         m |= m >> 8;
         return __builtin_amdgcn_readfirstlane((unsigned)(m & ((1u << NSG) - 1)));
     };
-#endif
     level_table(ntiles, off_s, cnt_s, lane);
     int sp = 0;
     if (lane == 0) stk[0] = ((bvh.levels - 1) << 26) | 0;
@@ -930,12 +917,8 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
             if (!__any(needs_vals(a, bb, bxt[0]))) continue;
         }
         if (lev > 0) {
-#if HDB_BOR_SUBTEST
             push_children_sub<D>(bvh, off_s, cnt_s, lev, idx, qlo, qhi, stk, sp, lane, bxs, bxt, sub_ok(sub_bound()),
                                  needs_vals, prof);
-#else
-            push_children<D>(bvh, off_s, cnt_s, lev, idx, qlo, qhi, stk, sp, lane, bxs, bxt, needs_vals);
-#endif
             continue;
         }
         // leaf: tile idx, 4 groups of 16 candidates.  The tile's records are fetched with one
@@ -953,15 +936,8 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
             staged_box<D, NSG>(bxs, gi, a, bb);
             return needs_vals(a, bb, bxt[gi]);
         };
-#if HDB_BOR_SUBTEST
         const unsigned gmask = group_mask();  // pre-filter; the per-lane test below decides
         prof.mark(6);
-#else
-        unsigned gmask = 0;
-#pragma unroll 1
-        for (int gi = 0; gi < NSG; gi++)
-            if (__any(gneeds(gi))) gmask |= 1u << gi;
-#endif
         if (gmask == 0) continue;
 #pragma unroll 1
         for (int gi = 0; gi < NSG; gi++) {
@@ -1056,7 +1032,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
             }
         }
         prof.mark(7);
-        if (HDB_BOR_LEAF_PUBLISH == 2) {
+        {
             // wave-aggregated publish: when every lane with a better edge shares one component
             // (the late rounds' common case), one DPP minimum and at most one atomic per wave
             const bool pub = found && (b.w * b.w) * (1.0 + 1e-12) < cb2;
@@ -1075,10 +1051,6 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
         if (found) {
             const double c2 = (b.w * b.w) * (1.0 + 1e-12);
             if (c2 < cb2) {
-                const unsigned long long bw = (unsigned long long)dbits(b.w);
-                if (HDB_BOR_LEAF_PUBLISH == 1 &&
-                    bw < __hip_atomic_load(&comp_w[mcomp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                    atomicMin(&comp_w[mcomp], bw);
                 cb2 = c2;
                 if (b.w < cwv) cwv = b.w;
             }
