@@ -358,7 +358,11 @@ struct LogEnt {
 constexpr int S_CST = 192;  // per 32-candidate block: hc[32], cn[32] (float), c2[32], cn[32] (double)
 
 #ifndef HDB_K1S_WAVES
-#define HDB_K1S_WAVES 8  // waves per workgroup (A/B: 4 waves x 2 query tiles, 56.0 vs 51.9 ms at C4)
+// waves per workgroup.  The block loop's one barrier per 32-candidate block makes every wave
+// wait for the slowest one's hit path; two 4-wave workgroups per CU (128 queries each) wait
+// on fewer waves and independently: screen 33.0 -> 31.1 ms at C4 (r05; round 3 measured 8
+// against 4 waves x 2 query tiles: 51.9 vs 56.0 ms)
+#define HDB_K1S_WAVES 4
 #endif
 #ifndef HDB_K1S_QT
 #define HDB_K1S_QT 1  // query tiles per wave at DP <= 128 (64 fragment VGPRs: 4 waves per SIMD)
