@@ -639,60 +639,95 @@ __global__ void km_keys_kernel(const float *__restrict__ Y, const int *__restric
 
 // Ball of G consecutive rows of the order (FP64, scaled domain v = (x - mu) sc, exactly as
 // split_rows_kernel computes v): centre, radius and max norm, both rounded up.  One
-// workgroup per group.
+// workgroup per group; each wave walks every fourth row, a row's d values spread over the
+// lanes (coalesced 512-byte loads): column sums for the centre, then per row the squared
+// distance to the centre and the squared norm summed over the wave.  Any centre gives a valid
+// ball (the radius is measured from it); the 1e-12 padding covers the summation-order error.
+__device__ __forceinline__ double wave_sum_d(double v) {
+    v = v + dpp_d<DPP_XOR1>(v);
+    v = v + dpp_d<DPP_XOR2>(v);
+    v = v + dpp_d<DPP_HMIRROR>(v);
+    v = v + dpp_d<DPP_MIRROR>(v);  // every lane: its 16-lane row's sum
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)b, (uint32_t)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+    v = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]) +
+        __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);  // own row + its pair
+    const uint64_t b2 = __builtin_bit_cast(uint64_t, v);
+    const auto lo2 = __builtin_amdgcn_permlane32_swap((uint32_t)b2, (uint32_t)b2, false, false);
+    const auto hi2 = __builtin_amdgcn_permlane32_swap((uint32_t)(b2 >> 32), (uint32_t)(b2 >> 32), false, false);
+    return __builtin_bit_cast(double, ((uint64_t)hi2[0] << 32) | lo2[0]) +
+           __builtin_bit_cast(double, ((uint64_t)hi2[1] << 32) | lo2[1]);
+}
+
 __global__ __launch_bounds__(256) void ball_kernel(const double *__restrict__ X, int d, const double *__restrict__ mu,
                                                    const double *__restrict__ prm, const int *__restrict__ perm,
                                                    const int *__restrict__ g_blk, const int *__restrict__ g_nblk,
                                                    int64_t G, int DPc, double *__restrict__ ctr,
                                                    double *__restrict__ rn) {
-    __shared__ double m_s[256];
-    __shared__ double r_s[256], q_s[256];
-    const int tid = threadIdx.x;
+    __shared__ double m_s[256], part_s[4][256];
+    __shared__ double r_s[4], q_s[4];
+    __shared__ int cnt_s[4];
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const double sc = prm[1];
     // rows [r0, r1) of the layout (padding rows, perm < 0, are not part of the ball)
     const int64_t r0 = g_blk ? (int64_t)g_blk[blockIdx.x] * 32 : (int64_t)blockIdx.x * G;
     const int64_t r1 = g_blk ? r0 + (int64_t)g_nblk[blockIdx.x] * 32 : r0 + G;
-    int64_t cnt = 0;
-    for (int64_t r = r0; r < r1; r++) cnt += perm[r] >= 0;
-    if (cnt == 0) {
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};  // columns lane + 64 j (d <= 256)
+    int cnt = 0;
+    for (int64_t r = r0 + wv; r < r1; r += 4) {
+        const int p = perm[r];  // wave-uniform
+        if (p < 0) continue;
+        cnt++;
+        const double *x = X + (int64_t)p * d;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int c = lane + 64 * j;
+            if (c < d) acc[j] += (x[c] - mu[c]) * sc;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (lane + 64 * j < d) part_s[wv][lane + 64 * j] = acc[j];
+    if (lane == 0) cnt_s[wv] = cnt;
+    __syncthreads();
+    const int tot = cnt_s[0] + cnt_s[1] + cnt_s[2] + cnt_s[3];
+    if (tot == 0) {
         for (int c = tid; c < DPc; c += 256) ctr[(int64_t)blockIdx.x * DPc + c] = 0.0;
         if (tid == 0) rn[2 * blockIdx.x] = rn[2 * blockIdx.x + 1] = 0.0;
         return;
     }
-    for (int c = tid; c < d; c += 256) {
-        double sum = 0.0;
-        for (int64_t r = r0; r < r1; r++)
-            if (perm[r] >= 0) sum += (X[(int64_t)perm[r] * d + c] - mu[c]) * sc;
-        m_s[c] = sum / (double)cnt;
-    }
+    for (int c = tid; c < d; c += 256) m_s[c] = (((part_s[0][c] + part_s[1][c]) + part_s[2][c]) + part_s[3][c]) / (double)tot;
     __syncthreads();
     for (int c = tid; c < DPc; c += 256) ctr[(int64_t)blockIdx.x * DPc + c] = c < d ? m_s[c] : 0.0;
     double md = 0.0, mn = 0.0;
-    for (int64_t r = r0 + tid; r < r1; r += 256) {
-        if (perm[r] < 0) continue;
-        const double *x = X + (int64_t)perm[r] * d;
+    for (int64_t r = r0 + wv; r < r1; r += 4) {
+        const int p = perm[r];
+        if (p < 0) continue;
+        const double *x = X + (int64_t)p * d;
         double a = 0.0, b = 0.0;
-        for (int c = 0; c < d; c++) {
-            const double v = (x[c] - mu[c]) * sc, e = v - m_s[c];
-            a += e * e;
-            b += v * v;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int c = lane + 64 * j;
+            if (c < d) {
+                const double v = (x[c] - mu[c]) * sc, e = v - m_s[c];
+                a += e * e;
+                b += v * v;
+            }
         }
-        md = fmax(md, a);
-        mn = fmax(mn, b);
+        md = fmax(md, wave_sum_d(a));
+        mn = fmax(mn, wave_sum_d(b));
     }
-    r_s[tid] = md;
-    q_s[tid] = mn;
+    if (lane == 0) {
+        r_s[wv] = md;
+        q_s[wv] = mn;
+    }
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (tid < o) {
-            r_s[tid] = fmax(r_s[tid], r_s[tid + o]);
-            q_s[tid] = fmax(q_s[tid], q_s[tid + o]);
-        }
-        __syncthreads();
-    }
     if (tid == 0) {
-        rn[2 * blockIdx.x] = sqrt(r_s[0]) * (1.0 + 1e-12) + 1e-300;
-        rn[2 * blockIdx.x + 1] = sqrt(q_s[0]) * (1.0 + 1e-12) + 1e-300;
+        const double R = fmax(fmax(r_s[0], r_s[1]), fmax(r_s[2], r_s[3]));
+        const double Q = fmax(fmax(q_s[0], q_s[1]), fmax(q_s[2], q_s[3]));
+        rn[2 * blockIdx.x] = sqrt(R) * (1.0 + 1e-12) + 1e-300;
+        rn[2 * blockIdx.x + 1] = sqrt(Q) * (1.0 + 1e-12) + 1e-300;
     }
 }
 
