@@ -1126,10 +1126,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(K1S_WPE
                         L[lcnt++] = e;
                     }
                     const float ub = f32_up(approx + bound);
-                    if (ub < tl[KT]) {  // insertion network (ascending)
+                    if (ub < tl[KT]) {  // insertion network (ascending): shift above the slot, ub into it
+                        bool lt[KR];
 #pragma unroll
-                        for (int k = KT; k > 0; k--) tl[k] = ub < tl[k - 1] ? tl[k - 1] : fminf(tl[k], ub);
-                        tl[0] = fminf(tl[0], ub);
+                        for (int k = 0; k < KR; k++) lt[k] = ub < tl[k];
+#pragma unroll
+                        for (int k = KT; k > 0; k--) tl[k] = lt[k - 1] ? tl[k - 1] : (lt[k] ? ub : tl[k]);
+                        tl[0] = lt[0] ? ub : tl[0];
                     }
                 }
             }
