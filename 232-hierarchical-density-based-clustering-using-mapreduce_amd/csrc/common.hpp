@@ -252,32 +252,34 @@ __device__ __forceinline__ void argmin_last(double &v, int &i, double v2, int i2
 
 // top-K insertion network (shared by K1, K1t and the epilogues)
 // Insert x into ascending buf[0..K) if x < buf[K-1] (strict, HDBSCANStar.java:89);
-// the largest element drops out.  Predicated compare/select chain, no dynamic indexing.
+// the largest element drops out.  x goes after every element <= x (ties keep the earlier
+// ones first), exactly where a bubble pass would put it; the K comparisons are independent
+// (buf is sorted, so lt[] is monotone) and every slot takes its value from one select pair --
+// no serial compare/carry chain, no dynamic indexing.
 template <int K>
 __device__ __forceinline__ void topk_insert(double (&buf)[K], double x) {
     if (x < buf[K - 1]) {
+        bool lt[K];
 #pragma unroll
-        for (int i = 0; i < K; i++) {
-            double b = buf[i];
-            bool lt = x < b;
-            buf[i] = lt ? x : b;
-            x = lt ? b : x;
-        }
+        for (int i = 0; i < K; i++) lt[i] = x < buf[i];
+#pragma unroll
+        for (int i = K - 1; i > 0; i--) buf[i] = lt[i - 1] ? buf[i - 1] : (lt[i] ? x : buf[i]);
+        buf[0] = lt[0] ? x : buf[0];
     }
 }
 template <int K>
 __device__ __forceinline__ void topk_insert_idx(double (&buf)[K], int (&idx)[K], double x, int xi) {
     if (x < buf[K - 1]) {
+        bool lt[K];
 #pragma unroll
-        for (int i = 0; i < K; i++) {
-            double b = buf[i];
-            int bi = idx[i];
-            bool lt = x < b;
-            buf[i] = lt ? x : b;
-            idx[i] = lt ? xi : bi;
-            x = lt ? b : x;
-            xi = lt ? bi : xi;
+        for (int i = 0; i < K; i++) lt[i] = x < buf[i];
+#pragma unroll
+        for (int i = K - 1; i > 0; i--) {
+            buf[i] = lt[i - 1] ? buf[i - 1] : (lt[i] ? x : buf[i]);
+            idx[i] = lt[i - 1] ? idx[i - 1] : (lt[i] ? xi : idx[i]);
         }
+        buf[0] = lt[0] ? x : buf[0];
+        idx[0] = lt[0] ? xi : idx[0];
     }
 }
 
