@@ -491,7 +491,10 @@ __device__ __noinline__ int log_compact(LogEnt *L, float t, int cap = S_LOGCAP) 
 // crowds 200 clusters together and every split cuts through dozens of them.)
 constexpr int KM_P = 32;   // projected dimensions
 constexpr int KM_K = 1024;  // centroids (several per cluster: a cluster without a seed merges)
-constexpr int KM_IT = 4;   // Lloyd iterations
+// Lloyd iterations of the layout's k-means (the layout only steers pruning): A/B at C4 (r05,
+// profiles/r05/c4/ab_kmeans_it.log): 2 -> order 2.7 ms, screen 30.0; 3 -> 3.1 / 30.0;
+// 4 -> 3.5 / 29.9; 6 -> 4.3 / 30.0 -- the extra passes no longer buy screen time
+constexpr int KM_IT = 2;
 
 __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
     x ^= x >> 16;
