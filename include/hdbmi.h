@@ -94,7 +94,9 @@ int hdb_ctx_synchronize(hdb_ctx *ctx);
  *                                  "prim_coop_xcd" (default 1: the plain attempt's working
  *                                  workgroups, when the run-time XCC_ID check finds them on one
  *                                  XCD, exchange through that XCD's L2 -- placement changes only
- *                                  speed), "prim_coop_slots" (exchange layout);
+ *                                  speed), "prim_coop_slots" (exchange layout; 6: the speculative
+ *                                  multi-step kernel, bit-exact, faster alone, slower when several
+ *                                  Prims share the GPU);
  *   "bubble_knn_split"(default 1): bubble core distances scan their candidates in chunks and
  *                                  replay the sequential insertion log exactly;
  *   "boruvka_seed"    (default 1): a Boruvka round starts from the previous round's still
@@ -106,6 +108,13 @@ int hdb_ctx_synchronize(hdb_ctx *ctx);
  *   "boruvka_wave_pts" (default 64; 16/32/64): points per scan wave; "boruvka_early_pts" /
  *                                  "boruvka_early_rounds": another size for the first rounds;
  *   "trav_pop_test"   (default 0): bit 0 Boruvka, bit 1 K1t re-test a popped node;
+ *   "ssort"           (default 1): the Morton order, the MST edge orders, K6's term order and
+ *                                  hdb_sort_edges_desc use the sample sort (unique 128-bit keys:
+ *                                  the same orders as the rocPRIM radix path, 0); "ssort_cap"
+ *                                  (default 0 = 4096: keys per bucket sorted in LDS; larger
+ *                                  buckets are merged in global memory);
+ *   "flat_relabel"    (default 1): hdb_flat_labels renumbers vertex labels in rank order first
+ *                                  (locality of the label records; the labels are unchanged);
  *   "count_evals"     (default 0): K1t/K2b count the pairs they evaluate (read "last_evals"). */
 int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value);
 /* Diagnostic counters: "last_evals" = pair evaluations of the last K1t call (count_evals on). */
