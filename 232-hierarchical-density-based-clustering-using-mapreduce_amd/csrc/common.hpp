@@ -42,6 +42,11 @@ struct Arena {  // grow-only device scratch, stream ordered reuse
     size_t bytes = 0;
 };
 
+struct StageChunk {  // Stager device memory: per-context chunks used as a stack
+    void *ptr = nullptr;
+    size_t bytes = 0, used = 0;
+};
+
 }  // namespace hdb
 
 struct hdb_ctx {
@@ -55,6 +60,8 @@ struct hdb_ctx {
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, std::pair<double, int64_t>> acc;
     hdb::Arena arenas[16];
+    std::vector<hdb::StageChunk> stage;  // Stager buffers (stack discipline, see Stager)
+    int stage_depth = 0;                 // live Stagers on this context
     int64_t *pinned = nullptr;  // pinned_words(): async device -> host counters
     void *host_stage = nullptr;  // host_arena(): grow-only pinned staging
     size_t host_stage_bytes = 0;
@@ -138,9 +145,14 @@ struct KernelTimer {
 bool is_device_ptr(const void *p);
 
 // Staging of caller arrays: device pointers pass through, host pointers are copied.
+// Device copies come from the context's own stage chunks, carved as a stack (a Stager frees
+// what it carved when it ends; nested Stagers carve above their parent), reused stream-ordered
+// on ctx->stream like the arenas.  No stream-ordered allocator (hipMallocAsync/hipFreeAsync on
+// the device's shared default pool) on this path: the C3/C5 model pool calls it from many host
+// threads at once, and per-context memory keeps those threads from sharing any allocator state.
 class Stager {
    public:
-    explicit Stager(hdb_ctx *ctx) : ctx_(ctx) {}
+    explicit Stager(hdb_ctx *ctx);
     ~Stager();
     // input array (nullable)
     template <class T>
@@ -164,7 +176,9 @@ class Stager {
    private:
     const void *in_raw(const void *p, size_t bytes);
     void *out_raw(void *p, size_t bytes, bool copy_in);
+    void *carve(size_t bytes);
     hdb_ctx *ctx_;
+    size_t mark_chunks_ = 0, mark_used_ = 0;
     struct Buf {
         void *dev;
         void *host_dst;

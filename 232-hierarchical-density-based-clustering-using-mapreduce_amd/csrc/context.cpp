@@ -1,8 +1,42 @@
 // context.cpp -- hdb_ctx lifetime, scratch arenas, kernel timing, host/device staging.
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <cstdlib>
+
 #include "common.hpp"
 
 namespace hdb {
+
+// Opt-in native backtrace on a fatal signal (HDB_NATIVE_BACKTRACE=1, set by bench.py): the
+// library's frames go to stderr, then the previous handler (Python's faulthandler, which dumps
+// every thread's Python stack, or the default action) runs.  Off by default: a JVM host uses
+// SIGSEGV itself (implicit null checks), so a library must not take it unasked.
+static struct sigaction g_prev_act[32];
+static void native_backtrace(int sig) {
+    static const char head[] = "\n[hdbmi] fatal signal, native backtrace:\n";
+    (void)!write(2, head, sizeof(head) - 1);
+    void *fr[64];
+    const int n = backtrace(fr, 64);
+    backtrace_symbols_fd(fr, n, 2);
+    sigaction(sig, &g_prev_act[sig], nullptr);
+    raise(sig);
+}
+__attribute__((constructor)) static void install_native_backtrace() {
+    const char *e = getenv("HDB_NATIVE_BACKTRACE");
+    if (!e || atoi(e) == 0) return;
+    void *warm[2];
+    (void)backtrace(warm, 2);  // loads libgcc's unwinder now, not inside the handler
+    for (int sig : {SIGSEGV, SIGBUS, SIGILL, SIGFPE, SIGABRT}) {
+        struct sigaction sa {};
+        sa.sa_handler = native_backtrace;
+        sigemptyset(&sa.sa_mask);
+        sa.sa_flags = SA_RESETHAND;
+        sigaction(sig, &sa, &g_prev_act[sig]);
+    }
+}
 
 static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
@@ -103,17 +137,56 @@ bool is_device_ptr(const void *p) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
+Stager::Stager(hdb_ctx *ctx) : ctx_(ctx) {
+    mark_chunks_ = ctx->stage.size();
+    mark_used_ = mark_chunks_ ? ctx->stage.back().used : 0;
+    ctx->stage_depth++;
+}
+
+// carve from the top chunk; a new chunk (at least twice the last) when it does not fit.  Chunks
+// are never freed while a Stager lives: queued copies and kernels may still use them
+void *Stager::carve(size_t bytes) {
+    const size_t nb = (std::max<size_t>(bytes, 16) + 255) & ~size_t(255);
+    auto &ch = ctx_->stage;
+    if (ch.empty() || ch.back().bytes - ch.back().used < nb) {
+        const size_t want = std::max<size_t>(nb, ch.empty() ? (size_t)1 << 20 : 2 * ch.back().bytes);
+        StageChunk c;
+        HIP_CHECK(hipMalloc(&c.ptr, want));
+        c.bytes = want;
+        ch.push_back(c);
+    }
+    void *p = (char *)ch.back().ptr + ch.back().used;
+    ch.back().used += nb;
+    return p;
+}
+
 Stager::~Stager() {
-    for (auto &b : bufs_)
-        if (b.dev) (void)hipFreeAsync(b.dev, ctx_->stream);
+    auto &ch = ctx_->stage;
+    // pop this Stager's carvings: chunks it added keep their memory (stream-ordered reuse)
+    for (size_t i = mark_chunks_; i < ch.size(); i++) ch[i].used = 0;
+    if (mark_chunks_) ch[mark_chunks_ - 1].used = mark_used_;
+    if (--ctx_->stage_depth == 0 && ch.size() > 1) {
+        // outermost Stager and the stack grew: fold the chunks into one of their total size
+        // once the stream has drained (the next call's carvings then never straddle chunks)
+        size_t total = 0;
+        for (auto &c : ch) total += c.bytes;
+        if (hipStreamSynchronize(ctx_->stream) == hipSuccess) {
+            for (auto &c : ch) (void)hipFree(c.ptr);
+            ch.clear();
+            StageChunk c;
+            if (hipMalloc(&c.ptr, total) == hipSuccess) {
+                c.bytes = total;
+                ch.push_back(c);
+            }
+        }
+    }
 }
 
 const void *Stager::in_raw(const void *p, size_t bytes) {
     if (!p) return nullptr;
     if (is_device_ptr(p)) return p;
     any_host_ = true;
-    void *d = nullptr;
-    HIP_CHECK(hipMallocAsync(&d, bytes ? bytes : 16, ctx_->stream));
+    void *d = carve(bytes);
     bufs_.push_back({d, nullptr, bytes});
     if (bytes) HIP_CHECK(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx_->stream));
     return d;
@@ -123,8 +196,7 @@ void *Stager::out_raw(void *p, size_t bytes, bool copy_in) {
     if (!p) return nullptr;
     if (is_device_ptr(p)) return p;
     any_host_ = true;
-    void *d = nullptr;
-    HIP_CHECK(hipMallocAsync(&d, bytes ? bytes : 16, ctx_->stream));
+    void *d = carve(bytes);
     bufs_.push_back({d, p, bytes});
     if (copy_in && bytes) HIP_CHECK(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx_->stream));
     return d;
@@ -203,6 +275,8 @@ void hdb_ctx_destroy(hdb_ctx *ctx) {
     for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
     for (auto &a : ctx->arenas)
         if (a.ptr) (void)hipFree(a.ptr);
+    for (auto &c : ctx->stage)
+        if (c.ptr) (void)hipFree(c.ptr);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->host_stage) (void)hipHostFree(ctx->host_stage);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);

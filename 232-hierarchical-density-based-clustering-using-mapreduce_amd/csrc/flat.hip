@@ -1402,8 +1402,10 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     const int64_t m = n - 1;  // a spanning tree has exactly n - 1 non-self edges
     int64_t *pin = pinned_words(ctx) + PINNED_WORDS - 8;  // private slice
     const int64_t mm = std::max<int64_t>(m, 1);
-    // vertex labels of the divide and conquer: rank-ordered (2m of them) or the point ids
-    const bool relabel = ctx->flat_relabel && m >= 1;
+    // vertex labels of the divide and conquer: rank-ordered (2m of them) or the point ids.
+    // Contracted labels are nv + rank: < 3m with relabelling (< 2n without, which the n guard
+    // above covers), so relabelling needs 3m to fit int32 -- larger inputs keep point ids
+    const bool relabel = ctx->flat_relabel && m >= 1 && flat_relabel_fits(m);
     const int64_t nv = relabel ? 2 * mm : n;
 
     // scratch: sizes are fixed by n and ne

@@ -61,6 +61,8 @@ void exact_leaf_device(hdb_ctx *ctx, const double *X, int64_t n, int d, int min_
 void boruvka_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const double *core, int metric, int32_t *va,
                     int32_t *vb, double *w);
 
+// K6 rank-order vertex labels: contracted labels reach nv + rank < 3m, stored as int32
+inline bool flat_relabel_fits(int64_t m) { return m >= 0 && 3 * m < (int64_t)INT32_MAX; }
 // K6: global hierarchy + flat labels over a merged MST (flat.hip); synchronises
 void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, const double *w, int64_t ne, int64_t n,
                         int32_t mcs, int32_t *labels, int64_t *n_clusters);

@@ -310,10 +310,11 @@ __device__ __forceinline__ int64_t ss_count_less(const SKey *a, int64_t m, const
     return lo;
 }
 
+// buf_in and bufB are the same buffer at the call site (the chunked merge's second scratch is
+// the scatter output, read before it is overwritten): neither may be __restrict__
 template <class EmitF>
-__global__ __launch_bounds__(SS_BT) void ss_bucket(EmitF ef, const SKey *__restrict__ buf_in, SKey *__restrict__ bufA,
-                                                   SKey *__restrict__ bufB, const int32_t *__restrict__ start,
-                                                   int cap) {
+__global__ __launch_bounds__(SS_BT) void ss_bucket(EmitF ef, const SKey *buf_in, SKey *__restrict__ bufA,
+                                                   SKey *bufB, const int32_t *__restrict__ start, int cap) {
     __shared__ SKey s[SS_CAP];
     const int64_t s0 = start[blockIdx.x], m = start[blockIdx.x + 1] - s0;
     if (m <= 0) return;

@@ -108,6 +108,11 @@ class MRHDBSCANStar:
         self._lvl = None
         self._t0 = None
         self._progress = bool(os.environ.get("HDB_PROGRESS"))  # one stderr line per level
+        # a fatal signal in any thread (the model pool drives the library from several) leaves
+        # every thread's Python stack on stderr; cheap, so always armed
+        import faulthandler
+        if not faulthandler.is_enabled():
+            faulthandler.enable(all_threads=True)
 
     def _mark(self, phase):
         """profile: phase wall time since the previous mark (synchronising); returns it"""

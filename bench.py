@@ -40,9 +40,14 @@ import numpy as np
 # driver runs concurrent local-model threads; with HIP's default of 4 queues several streams
 # share one queue and their kernels serialise (C2: 6.63 -> 6.1 ms/step with 8,
 # profiles/r05/hwq/).  Never above the pool's limit of 32.
-HW_QUEUES = min(32, int(os.environ.get("HDB_HW_QUEUES", "8")))  # (HDB_HW_QUEUES: A/B override)
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < HW_QUEUES:
-    os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
+# HDB_HW_QUEUES (> 0) is the explicit knob and wins in both directions.  Without it,
+# GPU_MAX_HW_QUEUES is raised to 8 but never lowered: the GPU pool exports
+# GPU_MAX_HW_QUEUES=4 (HIP's own default) into every job, so a value of 4 there is the
+# environment's, not a request for fewer queues.
+_hwq_req = int(os.environ.get("HDB_HW_QUEUES", "0") or 0)
+_hwq_env = int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)
+HW_QUEUES = min(32, _hwq_req if _hwq_req > 0 else max(8, _hwq_env))
+os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -1034,7 +1039,7 @@ def main():
         "data": "synthetic (seeded Gaussian blobs, 20 centers ~U[-100,100]^3, sigma 1, seed 1+rank)",
         "config": {"workload": "config 2: blobs 1M x 3 exact HDBSCAN* (no sampling), minPts 4, minClSize 4",
                    "points_per_gpu": n, "d": D, "min_pts": MIN_PTS, "min_cl_size": MIN_CL_SIZE,
-                   "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
+                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0),
                    "core": "EXCL_SELF", "timed": "X in pinned host memory -> H2D (each stage-1 worker uploads "
                    "its step's points on its own stream) -> K1t cores -> K2b MST + self edges, in the merge "
                    "order (HDB_EDGES_MERGED: tree edges sorted descending, self edges by core, one merge-path pass) "

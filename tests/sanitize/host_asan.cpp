@@ -155,6 +155,11 @@ static void local_model() {
 }
 
 int main() {
+    // K6 relabel limit (flat.hip): contracted labels nv + rank < 3m must fit int32
+    if (!hdb::flat_relabel_fits(715827882) || hdb::flat_relabel_fits(715827883) || !hdb::flat_relabel_fits(0)) {
+        printf("flat_relabel_fits limit wrong\n");
+        return 1;
+    }
     flat();
     formats();
     local_model();

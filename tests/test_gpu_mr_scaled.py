@@ -9,8 +9,9 @@
   merged list (the oracle's top-down flat labels are O(levels x n): hours at this size);
 * FULL-SIZE C3 (4M x 16) and C5 (16M x 8) exactly as bench.py runs them: property checks
   (2n - 1 edges, descending, the n - 1 tree edges span the points, one self edge per point,
-  every point processed by exactly one leaf, labels in 0..K) and the driver default
-  (prim_leaf_max 65,536) against the bench's prim_leaf_max 4,096 setting (same levels,
+  every point processed by exactly one leaf, labels in 0..K) and the driver default, which
+  the bench runs (prim_leaf_max 65,536: forced leaves up to 65,536 points take the reference
+  Prim, larger ones K2b), against prim_leaf_max 4,096 (K2b from 4,097 points; same levels,
   labels, weight multiset)."""
 import hashlib
 
@@ -102,7 +103,7 @@ def test_full_size_partitioned_config(pkg, name):
     lv = [(L["iteration"], sorted(L["leaves"].items()), sorted(L["big"].items()), L["new_keys"]) for L in got["levels"]]
     lab = got["labels"].cpu().numpy()
     del got
-    alt = pkg.MRHDBSCANStar(prim_leaf_max=4096, **kw).run(X)  # the bench's setting
+    alt = pkg.MRHDBSCANStar(prim_leaf_max=4096, **kw).run(X)  # more leaves on K2b
     assert [(L["iteration"], sorted(L["leaves"].items()), sorted(L["big"].items()), L["new_keys"])
             for L in alt["levels"]] == lv
     assert np.array_equal(alt["edges"][2].cpu().numpy(), w)
