@@ -64,12 +64,14 @@ __global__ void bubble_fold_dim_kernel(const double *__restrict__ X, int d, cons
     }
 }
 
-// per-bubble epilogue of the folded (LS, SS, n): exactly the tail of bubble_fold_kernel
+// per-bubble epilogue of the folded (LS, SS, n): exactly the tail of bubble_fold_kernel.
+// Member counts from the segment offsets, or (cntd != nullptr) from combined slice partials
 __global__ void bubble_epilogue_kernel(int d, const int64_t *__restrict__ off, int64_t nb, int variant,
                                        const double *__restrict__ ls, const double *__restrict__ ss,
-                                       double *__restrict__ rep, double *__restrict__ info) {
+                                       double *__restrict__ rep, double *__restrict__ info,
+                                       const double *__restrict__ cntd = nullptr) {
     HDB_GRID_STRIDE(b, nb) {
-        const int64_t cnt = off[b + 1] - off[b];
+        const int64_t cnt = cntd ? (int64_t)cntd[b] : off[b + 1] - off[b];
         const double *L = ls + b * d, *Q = ss + b * d;
         double *R = rep + b * d, *I = info + b * 3;
         if (cnt == 0) {
@@ -225,6 +227,140 @@ void bubble_stats_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const 
     HIP_CHECK(hipMemcpyAsync(&h_bad, bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
     if (h_bad) HDB_THROW(HDB_EINVAL, "bubble_of out of range");
+}
+
+// ---------------------------------------------- K4 over slices (D11)
+// CombineStep as Spark shapes it (reduceByKey: a map-side fold per partition, then the
+// partials merged; CombineStep.java:18-40 via Main.java:236-237) with the partitions fixed:
+// the rows are cut into S contiguous slices, each slice folds its members (ascending order,
+// the same chains as K4), and the partials of a bubble are combined in slice order.  A rank
+// folds only its own slices; the partials are gathered and combined in slice order on every
+// rank, so the result is the same at every rank count (oracle: orc_bubble_stats_combine_sliced).
+struct SliceCuts {
+    int64_t c[HDB_MAX_BUBBLE_SLICES + 1];
+    int S;
+};
+
+__global__ void slice_key_kernel(const int32_t *__restrict__ bo, int64_t n, int64_t nb, SliceCuts sc,
+                                 int32_t *__restrict__ key, int32_t *__restrict__ cnt, int *__restrict__ bad) {
+    HDB_GRID_STRIDE(i, n) {
+        const int32_t b = bo[i];
+        if (b < 0 || b >= nb) {
+            *bad = 1;
+            key[i] = 0;
+            continue;
+        }
+        int s = 0;
+        while (s + 1 < sc.S && i >= sc.c[s + 1]) s++;
+        const int32_t k = (int32_t)(s * nb + b);
+        key[i] = k;
+        atomicAdd(&cnt[k], 1);
+    }
+}
+
+__global__ void counts_to_double_kernel(const int64_t *__restrict__ off, int64_t m, double *__restrict__ out) {
+    HDB_GRID_STRIDE(k, m) out[k] = (double)(off[k + 1] - off[k]);
+}
+
+// per (bubble, dimension): the slice partials in slice order, empty slices skipped
+__global__ void bubble_combine_dim_kernel(const double *__restrict__ pls, const double *__restrict__ pss,
+                                          const double *__restrict__ pn, int S, int64_t nb, int d,
+                                          double *__restrict__ ls, double *__restrict__ ss) {
+    HDB_GRID_STRIDE(t, nb * d) {
+        const int64_t b = t / d;
+        double L = 0.0, Q = 0.0;
+        bool first = true;
+        for (int s = 0; s < S; s++) {
+            if (pn[(int64_t)s * nb + b] == 0) continue;
+            const double l = pls[(int64_t)s * nb * d + t], q = pss[(int64_t)s * nb * d + t];
+            L = first ? l : L + l;
+            Q = first ? q : Q + q;
+            first = false;
+        }
+        ls[t] = L;
+        ss[t] = Q;
+    }
+}
+
+__global__ void bubble_combine_n_kernel(const double *__restrict__ pn, int S, int64_t nb, double *__restrict__ n_out) {
+    HDB_GRID_STRIDE(b, nb) {
+        double c = 0;
+        for (int s = 0; s < S; s++) c += pn[(int64_t)s * nb + b];
+        n_out[b] = c;
+    }
+}
+
+void bubble_partials_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const int32_t *bo, int64_t nb,
+                            const int64_t *h_cuts, int S, double *pls, double *pss, double *pn) {
+    if (S < 1 || S > HDB_MAX_BUBBLE_SLICES) HDB_THROW(HDB_EINVAL, "bubble slices: 1..64");
+    if (h_cuts[0] != 0 || h_cuts[S] != n) HDB_THROW(HDB_EINVAL, "bubble slices: cuts must span [0, n]");
+    for (int s = 0; s < S; s++)
+        if (h_cuts[s + 1] < h_cuts[s]) HDB_THROW(HDB_EINVAL, "bubble slices: cuts must be non-decreasing");
+    if (n > INT32_MAX || (int64_t)S * nb > INT32_MAX) HDB_THROW(HDB_EINVAL, "bubble slices: too large");
+    const int64_t m = (int64_t)S * nb;
+    if (m <= 0) return;
+    SliceCuts sc{};
+    for (int s = 0; s <= S; s++) sc.c[s] = h_cuts[s];
+    sc.S = S;
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+        size_t o = off;
+        off += (bytes + 255) & ~size_t(255);
+        return o;
+    };
+    size_t o_key = carve(sizeof(int32_t) * (n + 1)), o_skey = carve(sizeof(int32_t) * (n + 1)),
+           o_perm = carve(sizeof(int32_t) * (n + 1)), o_iota = carve(sizeof(int32_t) * (n + 1)),
+           o_cnt = carve(sizeof(int32_t) * (m + 1)), o_off = carve(sizeof(int64_t) * (m + 1)), o_bad = carve(sizeof(int));
+    char *base = (char *)arena(ctx, A_WORK0, off);
+    int32_t *key = (int32_t *)(base + o_key), *skey = (int32_t *)(base + o_skey), *perm = (int32_t *)(base + o_perm),
+            *iota = (int32_t *)(base + o_iota), *cnt = (int32_t *)(base + o_cnt);
+    int64_t *offs = (int64_t *)(base + o_off);
+    int *bad = (int *)(base + o_bad);
+    const int g = 2048;
+    HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (m + 1), ctx->stream));
+    HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(int), ctx->stream));
+    KernelTimer t(ctx, "bubble_stats");
+    if (n > 0) {
+        hipLaunchKernelGGL(iota32_kernel, dim3(g), dim3(256), 0, ctx->stream, iota, n);
+        hipLaunchKernelGGL(slice_key_kernel, dim3(g), dim3(256), 0, ctx->stream, bo, n, nb, sc, key, cnt, bad);
+        int end_bit = 1;
+        while (end_bit < 32 && (int64_t(1) << end_bit) < m) end_bit++;
+        size_t tb = 0;
+        HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, skey, iota, perm, (int)n, 0, end_bit, ctx->stream));
+        void *tmp = arena(ctx, A_SORT, tb);
+        HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, skey, iota, perm, (int)n, 0, end_bit, ctx->stream));
+    }
+    {
+        size_t tb = 0;
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, offs, (int)(m + 1), ctx->stream));
+        void *tmp = arena(ctx, A_SORT, tb);
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, offs, (int)(m + 1), ctx->stream));
+    }
+    // a (slice, bubble) segment is a slice's members of the bubble in row order: K4's fold
+    hipLaunchKernelGGL(bubble_fold_dim_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(m * d, 256), 16384)), dim3(256),
+                       0, ctx->stream, X, d, perm, offs, m, pls, pss);
+    hipLaunchKernelGGL(counts_to_double_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(m, 256), 4096)), dim3(256), 0,
+                       ctx->stream, offs, m, pn);
+    HIP_CHECK(hipGetLastError());
+    int *pin = (int *)(pinned_words(ctx) + PINNED_WORDS - 40);
+    HIP_CHECK(hipMemcpyAsync(pin, bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (*pin) HDB_THROW(HDB_EINVAL, "bubble_of out of range");
+}
+
+void bubble_combine_device(hdb_ctx *ctx, const double *pls, const double *pss, const double *pn, int S, int64_t nb,
+                           int d, double *ls, double *ss, double *rep, double *info) {
+    if (S < 1) HDB_THROW(HDB_EINVAL, "bubble slices: S >= 1");
+    if (nb <= 0) return;
+    double *cntd = (double *)arena(ctx, A_WORK1, sizeof(double) * nb);
+    KernelTimer t(ctx, "bubble_combine");
+    hipLaunchKernelGGL(bubble_combine_dim_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(nb * d, 256), 16384)),
+                       dim3(256), 0, ctx->stream, pls, pss, pn, S, nb, d, ls, ss);
+    hipLaunchKernelGGL(bubble_combine_n_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(nb, 256), 4096)), dim3(256), 0,
+                       ctx->stream, pn, S, nb, cntd);
+    hipLaunchKernelGGL(bubble_epilogue_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(nb, 64), 4096)), dim3(64), 0,
+                       ctx->stream, d, nullptr, nb, (int)HDB_BUBBLE_COMBINESTEP, ls, ss, rep, info, cntd);
+    HIP_CHECK(hipGetLastError());
 }
 
 // ------------------------------------------------------------ K5 bubble kNN

@@ -291,6 +291,37 @@ int hdb_bubble_stats(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const 
     });
 }
 
+int hdb_bubble_partials(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const int32_t *bubble_of, int64_t nb,
+                        const int64_t *cuts, int32_t S, double *part_ls, double *part_ss, double *part_n) {
+    return guarded(ctx, [&] {
+        if (n < 0 || nb < 0 || d <= 0 || (!X && n) || (!bubble_of && n) || !cuts || !part_ls || !part_ss || !part_n)
+            HDB_THROW(HDB_EINVAL, "bad arguments");
+        if (S < 1 || S > HDB_MAX_BUBBLE_SLICES) HDB_THROW(HDB_EINVAL, "bubble slices: 1..HDB_MAX_BUBBLE_SLICES");
+        std::vector<int64_t> h_cuts = to_host(ctx, cuts, (size_t)S + 1);
+        Stager s(ctx);
+        const double *dX = s.in(X, n * d);
+        const int32_t *dbo = s.in(bubble_of, n);
+        double *pl = s.out(part_ls, (int64_t)S * nb * d), *pq = s.out(part_ss, (int64_t)S * nb * d),
+               *pn = s.out(part_n, (int64_t)S * nb);
+        bubble_partials_device(ctx, dX, n, d, dbo, nb, h_cuts.data(), S, pl, pq, pn);
+        s.finish();
+    });
+}
+
+int hdb_bubble_combine(hdb_ctx *ctx, const double *part_ls, const double *part_ss, const double *part_n, int32_t S,
+                       int64_t nb, int32_t d, double *ls, double *ss, double *rep, double *info) {
+    return guarded(ctx, [&] {
+        if (nb < 0 || d <= 0 || S < 1 || !part_ls || !part_ss || !part_n || !ls || !ss || !rep || !info)
+            HDB_THROW(HDB_EINVAL, "bad arguments");
+        Stager s(ctx);
+        const double *pl = s.in(part_ls, (int64_t)S * nb * d), *pq = s.in(part_ss, (int64_t)S * nb * d),
+                     *pn = s.in(part_n, (int64_t)S * nb);
+        double *dls = s.out(ls, nb * d), *dss = s.out(ss, nb * d), *drep = s.out(rep, nb * d), *dinfo = s.out(info, nb * 3);
+        bubble_combine_device(ctx, pl, pq, pn, S, nb, d, dls, dss, drep, dinfo);
+        s.finish();
+    });
+}
+
 static void bubble_core_impl(hdb_ctx *ctx, const double *rep, const int32_t *nB, const double *eB, const double *nnB,
                              int64_t b, int32_t d, int32_t min_pts, int32_t metric, std::vector<double> &core_h) {
     const int K = min_pts - 1;

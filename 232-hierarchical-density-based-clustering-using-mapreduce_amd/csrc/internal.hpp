@@ -37,6 +37,10 @@ void nearest_sample_device(hdb_ctx *ctx, const double *X, int64_t n, const doubl
                            const int32_t *xkey, const int32_t *skey, int32_t *out_i, double *out_d);
 void bubble_stats_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const int32_t *bo, int64_t nb, int variant,
                          double *ls, double *ss, double *rep, double *info);
+void bubble_partials_device(hdb_ctx *ctx, const double *X, int64_t n, int d, const int32_t *bo, int64_t nb,
+                            const int64_t *h_cuts, int S, double *pls, double *pss, double *pn);
+void bubble_combine_device(hdb_ctx *ctx, const double *pls, const double *pss, const double *pn, int S, int64_t nb,
+                           int d, double *ls, double *ss, double *rep, double *info);
 void bubble_knn_device(hdb_ctx *ctx, const double *rep, const double *eB, const double *nnB, int64_t b, int d,
                        int metric, int K, double *knn_out, int32_t *log_out);
 void sort_edges_desc_device(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne);

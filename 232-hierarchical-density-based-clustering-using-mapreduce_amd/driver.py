@@ -48,6 +48,7 @@ from .hdbscanstar import metric_of
 LEAF_PRIM_MAX = 65536  # leaves up to this size run the exact reference Prim (batched; one
 #                       workgroup per leaf <= 4096 points, one cooperative launch above)
 BORUVKA_DIMS = (1, 2, 3, 4, 8, 16)  # d with a K1t/K2b instantiation (csrc/spatial.hip)
+BUBBLE_SLICES = 8  # D11: CombineStep partials per fixed row slice (a rank folds only its slices)
 
 
 def boruvka_ok(metric: int, d: int, min_pts: int) -> bool:
@@ -70,7 +71,7 @@ class MRHDBSCANStar:
     def __init__(self, minPts=4, minClSize=4, processing_units=50, k=0.2, samples_per_subset=None,
                  seed=20210101, distanceFunction=None, all_inter_edges=True, max_levels=64, ctx=None,
                  device=0, flat_labels=True, profile=False, exact_prim_leaves=False, group=None,
-                 prim_leaf_max=LEAF_PRIM_MAX, model_threads=4, defer_leaves=True):
+                 prim_leaf_max=LEAF_PRIM_MAX, model_threads=4, defer_leaves=True, bubble_slices=BUBBLE_SLICES):
         self.minPts = minPts
         self.minClSize = minClSize
         self.processing_units = processing_units
@@ -100,6 +101,14 @@ class MRHDBSCANStar:
         # whole job (global LPT over the ranks, one batched Prim launch for every small leaf)
         # instead of one synchronising batch per level -- the same blocks, the same result
         self.defer_leaves = defer_leaves
+        # D11 (oracle/mr_driver.py): a level's big-subset rows are cut into this many fixed
+        # slices; CombineStep folds each slice and merges the partials in slice order (Spark's
+        # map-side combine per partition, Main.java:236-237, with the partitions fixed).  A rank
+        # folds only its own slices, so the statistics shard; 1 = one sequential fold (the
+        # round-1..5 order; the committed C1 / scaled-C5 fixtures were made with it)
+        self.bubble_slices = int(bubble_slices)
+        if not 1 <= self.bubble_slices <= 64:
+            raise ValueError("bubble_slices: 1..64")
         self._pool = None
         self.group = group      # torch.distributed group (None: the default group, if any)
         self._comm = None       # HdbComm for the merge under nccl
@@ -331,9 +340,12 @@ class MRHDBSCANStar:
             ls = torch.empty((nb, d), dtype=torch.float64, device=dev)
             ss, rep = torch.empty_like(ls), torch.empty_like(ls)
             info = torch.empty((nb, 3), dtype=torch.float64, device=dev)
-            A.check(A.lib().hdb_bubble_stats(c.h, Xb.data_ptr(), Xb.shape[0], d, nearest.data_ptr(), nb,
-                                             A.BUBBLE_COMBINESTEP, ls.data_ptr(), ss.data_ptr(), rep.data_ptr(),
-                                             info.data_ptr()), "CombineStep")
+            if self.bubble_slices > 1:
+                self._bubbles_sliced(c, Xb, nearest, nb, world, rank, ls, ss, rep, info)
+            else:
+                A.check(A.lib().hdb_bubble_stats(c.h, Xb.data_ptr(), Xb.shape[0], d, nearest.data_ptr(), nb,
+                                                 A.BUBBLE_COMBINESTEP, ls.data_ptr(), ss.data_ptr(), rep.data_ptr(),
+                                                 info.data_ptr()), "CombineStep")
             rep_h, info_h = rep.cpu().numpy(), info.cpu().numpy()
             if self.profile:
                 self._lvl["phase_s"]["bubbles"] = self._mark("bubbles")
@@ -461,6 +473,44 @@ class MRHDBSCANStar:
             out["n_clusters"] = int(k[0])
             self._mark("flat_labels")
         return out
+
+    def _bubbles_sliced(self, c, Xb, nearest, nb, world, rank, ls, ss, rep, info):
+        """D11 CombineStep: this rank's slices folded into partials (hdb_bubble_partials), the
+        partials of every rank gathered in rank (= slice) order, merged in slice order
+        (hdb_bubble_combine) -- the same statistics on every rank and at every world size."""
+        import torch
+        T, d = Xb.shape
+        Sl = self.bubble_slices
+        g = [T * s // Sl for s in range(Sl + 1)]          # parallel.chunk(T, Sl, s)
+        per = [P.chunk(Sl, world, r) for r in range(world)]  # slices of every rank
+        s0, s1 = per[rank]
+        k = s1 - s0
+        dev = Xb.device
+        pls = torch.empty(k * nb * d, dtype=torch.float64, device=dev)
+        pss = torch.empty_like(pls)
+        pn = torch.empty(k * nb, dtype=torch.float64, device=dev)
+        if k:
+            r0, r1 = g[s0], g[s1]
+            cuts = np.array([g[s] - r0 for s in range(s0, s1 + 1)], np.int64)
+            A.check(A.lib().hdb_bubble_partials(c.h, Xb[r0:r1].data_ptr(), r1 - r0, d, nearest[r0:r1].data_ptr(), nb,
+                                                cuts.ctypes.data, k, pls.data_ptr(), pss.data_ptr(), pn.data_ptr()),
+                    "CombineStep partials")
+        if world > 1:
+            mine = torch.cat([pls, pss, pn])
+            allp = P.allgather_var(mine, self.group).to(dev)
+            parts, o = [], 0
+            for r0_, r1_ in per:
+                kr = r1_ - r0_
+                sz = kr * nb * d
+                parts.append((allp[o:o + sz], allp[o + sz:o + 2 * sz], allp[o + 2 * sz:o + 2 * sz + kr * nb]))
+                o += 2 * sz + kr * nb
+            pls = torch.cat([p[0] for p in parts]).contiguous()
+            pss = torch.cat([p[1] for p in parts]).contiguous()
+            pn = torch.cat([p[2] for p in parts]).contiguous()
+        if self.profile:
+            self._lvl["phase_s"]["bubble_partials"] = self._mark("bubble_partials")
+        A.check(A.lib().hdb_bubble_combine(c.h, pls.data_ptr(), pss.data_ptr(), pn.data_ptr(), Sl, nb, d, ls.data_ptr(),
+                                           ss.data_ptr(), rep.data_ptr(), info.data_ptr()), "CombineStep merge")
 
     def _local_model(self, rep, info, threaded=False):
         """LocalModelReduceByKey.java:88-104 body (D4 ids) -> (labels, inter-cluster edges).

@@ -418,7 +418,8 @@ def predicted_scaling(drv, par, ns=(1, 2, 4, 8)):
     driver's own LPT on its own weights (n^2, b^2); a rank's phase time = the summed measured
     durations of its tasks x (phase wall time / summed task time at N = 1: the concurrency the
     model threads reach on one GPU), the phase = its slowest rank; the point-chunked nearest
-    sample scales as 1/N; bubbles (recomputed on every rank), bookkeeping, the merge and the
+    sample scales as 1/N, so do the bubble statistics' slice partials (D11: bubble_slices
+    slices, a rank folds its own); their merge, bookkeeping, the merge of the edge lists and the
     flat labels do not scale.  The driver's deferred leaves (every level's leaves in one
     batch after the level loop) are one more "level" holding only leaves, so their LPT runs
     over the whole job.  Not modelled: the all-gathers and the RCCL merge exchange."""
@@ -441,12 +442,15 @@ def predicted_scaling(drv, par, ns=(1, 2, 4, 8)):
                     load[o] += t
                 tot[kind] += float(load.max()) * wall / work
             tot["nearest_sample"] += ph.get("nearest_sample", 0.0) / N
-            tot["bubbles"] += ph.get("bubbles", 0.0)
+            # D11: the slice partials shard over the ranks (a rank folds its slices); the merge
+            # of the gathered partials and the host copy of rep / info do not
+            tot["bubbles"] += ph.get("bubble_partials", 0.0) / min(N, drv.bubble_slices) + ph.get("bubbles", 0.0)
         per[N] = {k: round(v, 3) for k, v in tot.items()} | {"fixed": round(fixed, 3)}
         out[N] = sum(tot.values()) + fixed
     return {"model": "LPT makespan of the measured N=1 task durations per level (local models; leaves "
                      "deferred: one LPT over the whole job), "
-                     "nearest sample / N, bubbles + bookkeeping + merge + flat labels unscaled; "
+                     "nearest sample / N, bubble slice partials / min(N, slices), their merge + "
+                     "bookkeeping + merge + flat labels unscaled; "
                      "all-gathers and the RCCL merge exchange not modelled",
             "seconds": {str(N): round(v, 3) for N, v in out.items()},
             "speedup": {str(N): round(out[1] / v, 2) for N, v in out.items()},
@@ -555,9 +559,9 @@ def run_partitioned(args, workload):
                 "data": f"synthetic (seeded Gaussian blobs, seed {cfg['seed']})",
                 "config": {"workload": cfg["desc"], "points": n, "d": cfg["d"], "min_pts": MIN_PTS,
                            "min_cl_size": MIN_CL_SIZE, "prim_leaf_max": drv.prim_leaf_max,
-                           "model_threads": drv.model_threads,
+                           "model_threads": drv.model_threads, "bubble_slices": drv.bubble_slices,
                            "parallelism": f"sharded driver x{world} (leaves/local models by LPT, "
-                                          f"point-chunked nearest sample, RCCL merge)"},
+                                          f"point-chunked nearest sample, sliced bubble partials, RCCL merge)"},
                 "iterations": r["iterations"], "n_clusters": r["n_clusters"],
                 "levels": len(lv), "leaves": int(sum(len(L["leaves"]) for L in lv)),
                 "model_errors": int(sum(len(L.get("model_errors", {})) for L in lv)),

@@ -55,6 +55,7 @@ extern "C" {
 /* Bubble-statistics variants */
 #define HDB_BUBBLE_COMBINESTEP 0 /* mappers/CombineStep.java:18-64 (live)            */
 #define HDB_BUBBLE_CF 1          /* datastructure/ClusterFeatureDataBubbles.java:192-215 */
+#define HDB_MAX_BUBBLE_SLICES 64 /* hdb_bubble_partials: slices per call                  */
 
 typedef struct hdb_ctx hdb_ctx;
 
@@ -196,6 +197,20 @@ int hdb_nearest_sample(hdb_ctx *ctx, const double *X, int64_t n, const double *S
  * Empty bubbles: all zero. */
 int hdb_bubble_stats(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const int32_t *bubble_of, int64_t nb,
                      int32_t variant, double *ls, double *ss, double *rep, double *info);
+
+/* CombineStep as Spark runs it: reduceByKey(new CombineStep()) (Main.java:236-237) folds each
+ * partition map-side, then merges the partials (CombineStep.java:18-40 on two partials).  With
+ * the partitions fixed (D11) the statistics shard: a rank folds the rows of its slices
+ * (cuts[0..S]: S + 1 non-decreasing row offsets, cuts[0] = 0, cuts[S] = n; S <= 64) into
+ * per-(slice, bubble) partials -- part_ls / part_ss: S x nb x d, part_n: S x nb member counts --
+ * and hdb_bubble_combine merges the gathered partials of all slices in slice order (empty
+ * partials skipped) and computes rep / extent / nnDist from the merged (LS, SS, n) with
+ * CombineStep.java:42-64's formulas.  One slice is hdb_bubble_stats(HDB_BUBBLE_COMBINESTEP)
+ * bit for bit. */
+int hdb_bubble_partials(hdb_ctx *ctx, const double *X, int64_t n, int32_t d, const int32_t *bubble_of, int64_t nb,
+                        const int64_t *cuts, int32_t S, double *part_ls, double *part_ss, double *part_n);
+int hdb_bubble_combine(hdb_ctx *ctx, const double *part_ls, const double *part_ss, const double *part_n, int32_t S,
+                       int64_t nb, int32_t d, double *ls, double *ss, double *rep, double *info);
 
 /* ------------------------------------------------------------- bubble model (a13-a15)
  * HdbscanDataBubbles.calculateCoreDistancesBubbles(double[][] repB, int[] nB, double[] eB,

@@ -336,6 +336,61 @@ int orc_bubble_stats_combine(const double *X, int64_t n, int d, const int32_t *b
     return ORC_OK;
 }
 
+/* CombineStep over SLICES (D11): the rows are cut into S contiguous slices (cuts[0..S], the
+ * driver's fixed slicing of a level's rows -- one or more slices per rank); every slice folds
+ * its members exactly as orc_bubble_stats_combine does (its partial: ls, ss, n), and the
+ * partials of a bubble are then combined in slice order, skipping slices without members:
+ * ls = ((p_a + p_b) + p_c) ..., ss likewise, n = the member count.  This is Spark's own shape
+ * for CombineStep (reduceByKey combines map-side per partition, Main.java:236-237, then merges
+ * the partials) with the partitions fixed, so the result does not depend on the rank count.
+ * rep / extent / nnDist come from the final (ls, ss, n) with CombineStep.java:42-64's formulas
+ * -- what its last call computes.  S = 1 is orc_bubble_stats_combine bit for bit. */
+int orc_bubble_stats_combine_sliced(const double *X, int64_t n, int d, const int32_t *bubble_of, int64_t nb,
+                                    const int64_t *cuts, int S, double *ls, double *ss, double *rep, double *info) {
+    if (S < 1 || cuts[0] != 0 || cuts[S] != n) return ORC_EINVAL;
+    for (int s = 0; s < S; s++)
+        if (cuts[s + 1] < cuts[s]) return ORC_EINVAL;
+    double *pl = (double *)malloc(sizeof(double) * (size_t)(nb * d));
+    double *pq = (double *)malloc(sizeof(double) * (size_t)(nb * d));
+    double *pr = (double *)malloc(sizeof(double) * (size_t)(nb * d));
+    double *pi = (double *)malloc(sizeof(double) * (size_t)(nb * 3));
+    if (!pl || !pq || !pr || !pi) {
+        free(pl), free(pq), free(pr), free(pi);
+        return ORC_EINVAL;
+    }
+    memset(ls, 0, sizeof(double) * (size_t)(nb * d));
+    memset(ss, 0, sizeof(double) * (size_t)(nb * d));
+    memset(info, 0, sizeof(double) * (size_t)(nb * 3));
+    int rc = ORC_OK;
+    for (int s = 0; s < S && rc == ORC_OK; s++) {
+        rc = orc_bubble_stats_combine(X + cuts[s] * d, cuts[s + 1] - cuts[s], d, bubble_of + cuts[s], nb, pl, pq, pr, pi);
+        for (int64_t b = 0; b < nb && rc == ORC_OK; b++) {
+            const double cnt = pi[b * 3 + 2];
+            if (cnt == 0) continue;
+            double *L = ls + b * d, *Q = ss + b * d;
+            if (info[b * 3 + 2] == 0) {
+                for (int i = 0; i < d; i++) { L[i] = pl[b * d + i]; Q[i] = pq[b * d + i]; }
+            } else {
+                for (int i = 0; i < d; i++) { L[i] = L[i] + pl[b * d + i]; Q[i] = Q[i] + pq[b * d + i]; }
+            }
+            info[b * 3 + 2] += cnt;
+        }
+    }
+    free(pl), free(pq), free(pr), free(pi);
+    if (rc != ORC_OK) return rc;
+    for (int64_t b = 0; b < nb; b++) {
+        double *L = ls + b * d, *Q = ss + b * d, *R = rep + b * d, *I = info + b * 3;
+        if (I[2] == 0) {
+            for (int i = 0; i < d; i++) R[i] = 0;
+            continue;
+        }
+        for (int i = 0; i < d; i++) R[i] = L[i] / I[2];  /* n = 1: x / 1 == x, the seed's rep */
+        I[0] = combine_extent(L, Q, I[2], d);           /* 0 when n = 1 */
+        I[1] = pow((1 / I[2]), (double)(1 / d)) * I[0];
+    }
+    return ORC_OK;
+}
+
 /* ClusterFeatureDataBubbles.calculateRep/Extent/Nndist (ClusterFeatureDataBubbles.java:192-215)
  * driven by ConstructDataBubblesReducer.call (ConstructDataBubblesReducer.java:74-90):
  * n = n1 + n2 (int), extent = sqrt(sum_i (2n*ss - 2ls^2) / (n*(n-1)))  with the int

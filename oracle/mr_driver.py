@@ -20,7 +20,12 @@ recursion can spin forever, Q11):
       becomes a forced leaf; after max_levels every subset is a leaf;
   D10 a local model that raises one of the reference's exceptions (e.g. Clusters.java:45-46,
       "Cluster cannot have less than 0 points") does not end the run: the subset is treated
-      as one label, i.e. a forced leaf (recorded in levels[i]["model_errors"]).
+      as one label, i.e. a forced leaf (recorded in levels[i]["model_errors"]);
+  D11 bubble_slices = S > 1: a level's big-subset rows (concatenated in key order, ascending
+      id inside a subset) are cut into S fixed contiguous slices (slice s = rows [T s / S,
+      T (s + 1) / S)); CombineStep folds each slice and combines the partials in slice order
+      (oracle.bubble_stats cuts=...) -- Spark's map-side combine per partition with the
+      partitions fixed; the product driver's sliced bubble statistics.  S = 1: one fold.
 """
 from __future__ import annotations
 
@@ -52,7 +57,7 @@ def _nearest_chunked(P, S, metric, pool, workers):
 
 
 def run(X, min_pts=4, min_cl_size=4, processing_units=50, k=0.2, samples_per_subset=None, seed=20210101,
-        metric="euclidean", all_inter_edges=True, max_levels=64, log=None, flat=True, workers=1):
+        metric="euclidean", all_inter_edges=True, max_levels=64, log=None, flat=True, workers=1, bubble_slices=1):
     """Returns dict(edges=(va, vb, w) merged (stable, descending weight), levels=[...],
     leaf_of=np.array subset key of the leaf that processed each point, iterations).
 
@@ -67,14 +72,22 @@ def run(X, min_pts=4, min_cl_size=4, processing_units=50, k=0.2, samples_per_sub
         pool = cf.ThreadPoolExecutor(workers)
     try:
         return _run(X, min_pts, min_cl_size, processing_units, k, samples_per_subset, seed, metric,
-                    all_inter_edges, max_levels, log, flat, pool, workers)
+                    all_inter_edges, max_levels, log, flat, pool, workers, bubble_slices)
     finally:
         if pool is not None:
             pool.shutdown()
 
 
+def slice_cuts(sizes, S):
+    """D11: per subset (sizes in key order), its local cuts of the level's S fixed slices"""
+    T = int(np.sum(sizes))
+    g = np.array([T * s // S for s in range(S + 1)], np.int64)  # parallel.chunk(T, S, s)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    return [np.clip(g - off[i], 0, sizes[i]) for i in range(len(sizes))]
+
+
 def _run(X, min_pts, min_cl_size, processing_units, k, samples_per_subset, seed, metric, all_inter_edges,
-         max_levels, log, flat, pool, workers):
+         max_levels, log, flat, pool, workers, bubble_slices=1):
     X = np.ascontiguousarray(X, np.float64)
     n, d = X.shape
     key_of = np.zeros(n, np.int64)            # MapperDataset_github.java:20: key 0
@@ -119,13 +132,15 @@ def _run(X, min_pts, min_cl_size, processing_units, k, samples_per_subset, seed,
         inter_edges = []
         new_alive = np.zeros(n, bool)
         new_key = np.full(n, -2, np.int64)
+        cuts_of = dict(zip(big_keys, slice_cuts([members[c].shape[0] for c in big_keys], bubble_slices))) \
+            if bubble_slices > 1 else {}
         def model(c):
             rows = members[c]
             sp = sample_ids(rows.shape[0], k, samples_per_subset, seed, iteration - 1, c)
             S = X[rows[sp]]
             nearest = _nearest_chunked(X[rows], S, metric, pool if len(big_keys) == 1 else None, workers)
             # CombineStep per (subset, sample): fold in ascending global id (D5)
-            st = O.bubble_stats(X[rows], nearest, S.shape[0], "combine")
+            st = O.bubble_stats(X[rows], nearest, S.shape[0], "combine", cuts=cuts_of.get(c))
             nonempty = np.nonzero(st["info"][:, 2] > 0)[0]  # D4 (a 1-member bubble keeps [0, 0, 1])
             lm, err = None, None
             if nonempty.shape[0] >= 2:

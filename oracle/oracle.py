@@ -57,6 +57,7 @@ def lib():
         L.orc_nearest_sample.argtypes = [dp, i64, dp, i64, i32, i32, ip, ip, ip, dp]
         L.orc_bubble_stats_combine.argtypes = [dp, i64, i32, ip, i64, dp, dp, dp, dp]
         L.orc_bubble_stats_cf.argtypes = [dp, i64, i32, ip, i64, dp, dp, dp, dp]
+        L.orc_bubble_stats_combine_sliced.argtypes = [dp, i64, i32, ip, i64, lp, i32, dp, dp, dp, dp]
         L.orc_distance_bubbles.restype = C.c_double
         L.orc_distance_bubbles.argtypes = [C.c_double, dp, dp, i64, i64]
         L.orc_bubble_core_distances.argtypes = [dp, ip, dp, dp, i64, i32, i32, i32, dp]
@@ -203,8 +204,10 @@ def nearest_sample(X, S, metric="euclidean", x_key=None, s_key=None):
     return nn, dist
 
 
-def bubble_stats(X, bubble_of, nb, variant="combine"):
+def bubble_stats(X, bubble_of, nb, variant="combine", cuts=None):
     """CombineStep (CombineStep.java:18-64) or CF (ClusterFeatureDataBubbles.java:192-215).
+    cuts (CombineStep only): S + 1 slice boundaries over the rows -- per-slice folds combined
+    in slice order (D11, orc_bubble_stats_combine_sliced); None: one sequential fold.
     Returns dict(ls, ss, rep, info) with info[:, (extent, nnDist, n)]."""
     X, px = _d(X)
     n, d = X.shape
@@ -213,6 +216,14 @@ def bubble_stats(X, bubble_of, nb, variant="combine"):
     ss = np.zeros((nb, d))
     rep = np.zeros((nb, d))
     info = np.zeros((nb, 3))
+    if cuts is not None:
+        if variant != "combine":
+            raise ValueError("slices apply to CombineStep only")
+        cu = np.ascontiguousarray(cuts, np.int64)
+        _chk(lib().orc_bubble_stats_combine_sliced(px, n, d, pb, nb, cu.ctypes.data_as(C.POINTER(C.c_int64)),
+                                                   cu.shape[0] - 1, _d(ls)[1], _d(ss)[1], _d(rep)[1], _d(info)[1]),
+             "bubble_stats_sliced")
+        return dict(ls=ls, ss=ss, rep=rep, info=info)
     fn = lib().orc_bubble_stats_combine if variant == "combine" else lib().orc_bubble_stats_cf
     _chk(fn(px, n, d, pb, nb, _d(ls)[1], _d(ss)[1], _d(rep)[1], _d(info)[1]), "bubble_stats")
     return dict(ls=ls, ss=ss, rep=rep, info=info)

@@ -58,7 +58,7 @@ def test_c1_full_skin_bit_exact(pkg, skin):
     assert skin.shape == (245057, 3)
     t0 = time.perf_counter()
     got = pkg.MRHDBSCANStar(minPts=4, minClSize=4, processing_units=50, k=0.2, seed=20210101,
-                            exact_prim_leaves=True).run(skin)
+                            exact_prim_leaves=True, bubble_slices=1).run(skin)  # the fixture's one fold
     va, vb, w = (x.cpu().numpy() for x in got["edges"])
     print(f"C1 full Skin (exact Prim leaves): {time.perf_counter() - t0:.2f} s")
     _check_structure(G, got)
@@ -73,7 +73,8 @@ def test_c1_full_skin_boruvka_leaf(pkg, skin):
     hierarchy removes a tie group at once, so it does not depend on which MST is used)."""
     G = golden("c1_skin_full")
     t0 = time.perf_counter()
-    got = pkg.MRHDBSCANStar(minPts=4, minClSize=4, processing_units=50, k=0.2, seed=20210101).run(skin)
+    got = pkg.MRHDBSCANStar(minPts=4, minClSize=4, processing_units=50, k=0.2, seed=20210101,
+                            bubble_slices=1).run(skin)
     print(f"C1 full Skin (Boruvka leaf): {time.perf_counter() - t0:.2f} s")
     _check_structure(G, got)
     va, vb, w = (x.cpu().numpy() for x in got["edges"])

@@ -11,13 +11,16 @@ pytestmark = pytest.mark.gpu
 
 
 def run_both(pkg, X, **kw):
+    """oracle and device on the same input; both fold CombineStep over the same slices (D11:
+    the driver's default, or bubble_slices given)"""
     from oracle import mr_driver as M
+    kw.setdefault("bubble_slices", pkg.driver.BUBBLE_SLICES)
     ref = M.run(X, **kw)
     got = pkg.MRHDBSCANStar(minPts=kw.get("min_pts", 4), minClSize=kw.get("min_cl_size", 4),
                             processing_units=kw["processing_units"], k=kw.get("k", 0.2),
                             samples_per_subset=kw.get("samples_per_subset"),
                             all_inter_edges=kw.get("all_inter_edges", True),
-                            distanceFunction=kw.get("metric")).run(X)
+                            distanceFunction=kw.get("metric"), bubble_slices=kw["bubble_slices"]).run(X)
     return ref, got
 
 

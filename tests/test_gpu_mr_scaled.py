@@ -29,7 +29,7 @@ def _scaled(pkg, **kw):
     mp, mcl, pu, sps, s2 = (int(x) for x in G["args"])
     X = blobs(n, d, centers, seed, spread=100.0)
     got = pkg.MRHDBSCANStar(minPts=mp, minClSize=mcl, processing_units=pu, samples_per_subset=sps, seed=s2,
-                            **kw).run(X)
+                            bubble_slices=1, **kw).run(X)  # the fixture was made with one CombineStep fold
     return G, got
 
 

@@ -295,6 +295,53 @@ def test_bubble_stats_cf(pkg):
     np.testing.assert_allclose(info[:, 1], g["cf_info"][:, 1], rtol=1e-9)  # real-exponent pow
 
 
+@pytest.mark.parametrize("d", [1, 3, 8])
+def test_bubble_partials_combine_vs_oracle_slices(pkg, oracle, d):
+    """D11 CombineStep over slices: hdb_bubble_partials (per-slice folds, here in two calls as
+    two ranks would make them) + hdb_bubble_combine (slice order, empty partials skipped) equal
+    the oracle's sliced fold bit for bit -- empty slices, a one-slice bubble, empty bubbles --
+    and one slice equals hdb_bubble_stats"""
+    import ctypes
+    import torch
+    A = pkg._capi
+    rng = np.random.default_rng(40 + d)
+    n, nb = 20000, 3000
+    X = np.round(rng.normal(size=(n, d)) * 30, 3)
+    bo = rng.integers(0, nb, n).astype(np.int32)
+    bo[bo == 11] = 12                           # bubble 11 empty
+    bo[bo == 2999] = 7
+    bo[5000:5003] = 2999                        # bubble 2999: three members, all in one slice
+    dev = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    c = A.Context.get(0)
+    c.use_torch_stream()
+    for cuts in ([0, n], [0, 2500, 2500, 9000, 13000, n], [0, 4000, 8000, 12000, 16000, n], [0, 0, n, n]):
+        S = len(cuts) - 1
+        pl = torch.empty(S * nb * d, dtype=torch.float64, device="cuda")
+        pq, pn = torch.empty_like(pl), torch.empty(S * nb, dtype=torch.float64, device="cuda")
+        h = S // 2  # slices [0, h) and [h, S) folded by two calls ("ranks")
+        for s0, s1 in ((0, h), (h, S)):
+            if s1 == s0:
+                continue
+            r0, r1 = cuts[s0], cuts[s1]
+            lc = np.array([cuts[s] - r0 for s in range(s0, s1 + 1)], np.int64)
+            Xd, bd = dev(X[r0:r1]), dev(bo[r0:r1])
+            A.check(A.lib().hdb_bubble_partials(c.h, Xd.data_ptr(), r1 - r0, d, bd.data_ptr(), nb, lc.ctypes.data,
+                                                s1 - s0, pl[s0 * nb * d:].data_ptr(), pq[s0 * nb * d:].data_ptr(),
+                                                pn[s0 * nb:].data_ptr()), "partials")
+        out = [torch.empty((nb, d), dtype=torch.float64, device="cuda") for _ in range(3)]
+        info = torch.empty((nb, 3), dtype=torch.float64, device="cuda")
+        A.check(A.lib().hdb_bubble_combine(c.h, pl.data_ptr(), pq.data_ptr(), pn.data_ptr(), S, nb, d,
+                                           *(o.data_ptr() for o in out), info.data_ptr()), "combine")
+        r = oracle.bubble_stats(X, bo, nb, cuts=cuts)
+        got = dict(ls=out[0], ss=out[1], rep=out[2], info=info)
+        for k in ("ls", "ss", "rep", "info"):
+            assert eq(got[k].cpu().numpy(), r[k]), (cuts, k)
+        if S == 1:
+            ls, ss, rep, inf = pkg.bubble_stats(X, bo, nb)
+            assert eq(rep, r["rep"]) and eq(inf, r["info"]) and eq(ls, r["ls"])
+    assert r["info"][11, 2] == 0 and r["info"][2999, 2] == 3
+
+
 def test_bubble_stats_empty_and_d1(pkg, oracle):
     X = np.random.default_rng(1).normal(size=(1000, 1))
     bo = np.random.default_rng(2).integers(0, 300, 1000).astype(np.int32)

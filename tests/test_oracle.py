@@ -273,3 +273,20 @@ def test_create_local_mst_record_fields(oracle):
     assert np.array_equal(ids[f1], va) and np.array_equal(ids[f2], vb) and np.all(nd == 11)
     n = X.shape[0]
     assert np.array_equal(f2[:n - 1], np.arange(n - 1)) and np.array_equal(f1[n - 1:], np.arange(n))
+
+
+def test_bubble_stats_slices_d11(oracle):
+    """D11: one slice is the sequential CombineStep fold bit for bit; any slicing keeps the
+    member counts and differs from the fold only by summation order (rounding)"""
+    rng = np.random.default_rng(3)
+    X = np.round(rng.normal(size=(6000, 5)) * 10, 3)
+    bo = rng.integers(0, 900, 6000).astype(np.int32)
+    a = oracle.bubble_stats(X, bo, 900)
+    b = oracle.bubble_stats(X, bo, 900, cuts=[0, 6000])
+    assert all(np.array_equal(a[k], b[k]) for k in a)
+    c = oracle.bubble_stats(X, bo, 900, cuts=[0, 0, 1500, 3000, 6000])
+    assert np.array_equal(a["info"][:, 2], c["info"][:, 2])
+    np.testing.assert_allclose(c["ls"], a["ls"], rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(c["rep"], a["rep"], rtol=1e-12, atol=1e-12)
+    with pytest.raises(oracle.OracleError):
+        oracle.bubble_stats(X, bo, 900, cuts=[0, 7000])
