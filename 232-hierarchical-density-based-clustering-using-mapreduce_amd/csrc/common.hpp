@@ -99,6 +99,7 @@ struct hdb_ctx {
     int flat_root_variant = 3;  // K6 dc_root A/B: 0 LDS table (256 threads), 1 (1024), 2 direct atomics, 3-5 multi-batch
     bool flat_relabel = true;  // K6: divide-and-conquer vertex labels in rank order (locality; false: point ids)
     int flat_block_log = 10;
+    int flat_mid_log = 12;     // K6: depths below 2^flat_mid_log ranks per workgroup (dc_mid, L2-local); <= block log: off
     int flat_deep_depth = 64;  // K6: global depths >= this use flat_deep_root / flat_deep_link (A/B)
     int flat_deep_root = 3;
     int flat_deep_link = 1;   // K6: deep depths per workgroup in LDS (2^x ranks, 8-10; 0: the sequential dc_local)
@@ -119,6 +120,7 @@ enum {
 };
 
 void *arena(hdb_ctx *ctx, int slot, size_t bytes);
+bool hdb_prim_spec_built();  // prim.hip: the speculative Prim (slots 6) is in this build
 constexpr int PINNED_WORDS = 512;
 int64_t *pinned_words(hdb_ctx *ctx);
 // grow-only pinned host buffer (synchronises the stream before it grows)

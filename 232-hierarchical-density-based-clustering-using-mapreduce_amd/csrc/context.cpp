@@ -238,7 +238,8 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         for (const char *k : {"prim_coop_plain_retries", "prim_coop_steps", "prim_coop_launches", "bubble_knn_replay_overflows",
                               "boruvka_visits_sum", "boruvka_evals_sum", "boruvka_bound_ns_sum"})
             c->stats[k] = 0;
-        if (const char *e = getenv("HDB_PRIM_COOP_SLOTS")) c->prim_coop_slots = atoi(e);  // A/B knob
+        if (const char *e = getenv("HDB_PRIM_COOP_SLOTS"))  // A/B knob
+            c->prim_coop_slots = (atoi(e) == 6 && !hdb_prim_spec_built()) ? 4 : atoi(e);
         // per-kernel HIP-event timing from birth (contexts created on worker threads, bench.py)
         if (const char *e = getenv("HDB_KERNEL_TIMING")) c->timing = atoi(e) != 0;
         if (const char *e = getenv("HDB_FLAT_BLOCK_LOG")) c->flat_block_log = atoi(e);  // A/B knob
@@ -252,6 +253,7 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         if (const char *e = getenv("HDB_SSORT")) c->ssort = atoi(e) != 0;                // A/B knob
         if (const char *e = getenv("HDB_FLAT_RELABEL")) c->flat_relabel = atoi(e) != 0;  // A/B knob
         if (const char *e = getenv("HDB_FLAT_DEEP")) c->flat_deep_depth = atoi(e);          // A/B knob
+        if (const char *e = getenv("HDB_FLAT_MID")) c->flat_mid_log = atoi(e);              // A/B knob
         if (const char *e = getenv("HDB_FLAT_DEEP_ROOT")) c->flat_deep_root = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_FLAT_DEEP_LINK")) c->flat_deep_link = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_BOR_EARLY_PTS")) c->boruvka_early_pts = atoi(e);    // A/B knob
@@ -404,6 +406,10 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
     }
     if (k == "prim_coop_slots") {
         if (value < 0 || value > 6) return HDB_EINVAL;
+        if (value == 6 && !hdb_prim_spec_built()) {  // csrc/prim.hip: only with -DHDB_PRIM_SPEC=1
+            set_error("prim_coop_slots 6: the speculative Prim is not in this build (-DHDB_PRIM_SPEC=1)");
+            return HDB_EUNSUPPORTED;
+        }
         ctx->prim_coop_slots = (int)value;
         return HDB_OK;
     }
@@ -439,6 +445,11 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
     }
     if (k == "boruvka_knn_seed") {
         ctx->boruvka_knn_seed = value != 0;
+        return HDB_OK;
+    }
+    if (k == "flat_mid_log") {
+        if (value < 0 || value > 24) return HDB_EINVAL;
+        ctx->flat_mid_log = (int)value;
         return HDB_OK;
     }
     if (k == "flat_relabel") {

@@ -513,6 +513,178 @@ __global__ __launch_bounds__(TB) void dc_link_multi(DC c, int b, int j, int64_t 
     }
 }
 
+// Middle depths in one launch (round 6): a workgroup owns a block of 2^LM consecutive ranks and
+// runs the global depths' four phases (dc_init, dc_unite, dc_root_multi, dc_link_multi: the
+// same per-edge work on the same global arrays) for its block's depths b = LM-1 .. LB itself,
+// one workgroup barrier between phases instead of a kernel boundary.  With rank-ordered labels
+// (flat_relabel) a block's label records, stamps and edge arrays are a few hundred KB, so they
+// stay in the one XCD's L2 the workgroup runs on -- a global depth spreads every block over all
+// eight XCDs and streams the whole record array through the MALL.  Cross-wave visibility of the
+// plain stores and the L2 atomics between phases: the workgroup barrier's workgroup-scope
+// acquire/release (every wave of the workgroup shares one CU and its write-through L1; the
+// compiler's gfx950 memory model needs no cache maintenance at that scope).  An agent-scope
+// __threadfence here would write the XCD's L2 back at every phase (buffer_wbl2): 4x slower.
+__device__ __forceinline__ void dc_phase_sync() { __syncthreads(); }
+
+template <int TB>
+__global__ __launch_bounds__(TB) void dc_mid(DC c, int J, int LM, int LB, int *__restrict__ err) {
+    constexpr int RS = 4096, KS = 8192;  // LDS table slots: root phase (4 ints), link phase (2 ints)
+    __shared__ int32_t tab[4 * RS > 2 * KS ? 4 * RS : 2 * KS];
+    __shared__ int s_used;
+    const int t = threadIdx.x;
+    const int64_t blk = blockIdx.x;
+    if ((blk << LM) >= c.m) return;
+    int e_cyc = 0;
+    for (int b = LM - 1; b >= LB; b--) {
+        const int j = J - 1 - b;
+        const int64_t bl = int64_t(1) << (b + 1), half = int64_t(1) << b;
+        const int64_t nl = (c.m / bl) * half + std::min(c.m % bl, half);
+        const int64_t i0 = blk << (LM - 1), i1 = std::min(i0 + (int64_t(1) << (LM - 1)), nl);
+        // init
+        for (int64_t i = i0 + t; i < i1; i += TB) {
+            const int64_t r = l_rank(i, b);
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const int32_t x = c.lab[2 * r + s];
+                c.lr[x] = LRec{x, -1, 0, NONE};
+                c.stamp[x] = 2 * j;
+            }
+        }
+        dc_phase_sync();
+        // unite
+        for (int64_t i = i0 + t; i < i1; i += TB) {
+            const int64_t r = l_rank(i, b);
+            const int32_t h = uf_unite(c.lr, c.lab[2 * r], c.lab[2 * r + 1], c.n);
+            c.hooked[r] = h;
+            if (h < 0) e_cyc = 1;
+        }
+        dc_phase_sync();
+        // root: per component largest L edge, summed sizes, smallest id (LDS-combined)
+        {
+            int32_t *skey = tab, *smax = tab + RS, *ssum = tab + 2 * RS, *smin = tab + 3 * RS;
+            auto clear = [&]() {
+                for (int k = t; k < RS; k += TB) {
+                    skey[k] = -1;
+                    smax[k] = -1;
+                    ssum[k] = 0;
+                    smin[k] = NONE;
+                }
+                if (t == 0) s_used = 0;
+            };
+            auto flush = [&]() {
+                for (int k = t; k < RS; k += TB) {
+                    const int32_t rep = skey[k];
+                    if (rep < 0) continue;
+                    atomicMax(&c.lr[rep].rootedge, smax[k]);
+                    if (ssum[k]) atomicAdd(&c.lr[rep].csize, ssum[k]);
+                    if (smin[k] != NONE) atomicMin(&c.lr[rep].cmin, smin[k]);
+                }
+            };
+            clear();
+            __syncthreads();
+            for (int64_t base = i0; base < i1; base += TB) {
+                const int64_t i = base + t;
+                if (i < i1) {
+                    const int64_t r = l_rank(i, b);
+                    const int32_t rep = uf_find(c.lr, c.lab[2 * r]);
+                    const int32_t x = c.hooked[r];
+                    c.hooked[r] = rep;
+                    const int32_t sz = x < 0 ? 0 : (x < c.n ? 1 : c.esize[x - c.n]);
+                    const int32_t mi = x < 0 ? NONE : (x < c.n ? vid(c, x) : c.eminid[x - c.n]);
+                    uint32_t h = uf_prio(rep, 0) & (RS - 1);
+                    while (true) {  // kept below RS / 2 keys before every batch of TB
+                        const int32_t k = atomicCAS(&skey[h], -1, rep);
+                        if (k == -1) {
+                            atomicAdd(&s_used, 1);
+                            break;
+                        }
+                        if (k == rep) break;
+                        h = (h + 1) & (RS - 1);
+                    }
+                    atomicMax(&smax[h], (int32_t)r);
+                    if (sz) atomicAdd(&ssum[h], sz);
+                    if (mi != NONE) atomicMin(&smin[h], mi);
+                }
+                __syncthreads();
+                if (base + TB < i1 && s_used > RS / 2 - TB) {
+                    flush();
+                    __syncthreads();
+                    clear();
+                    __syncthreads();
+                }
+            }
+            flush();
+        }
+        dc_phase_sync();
+        // link: root edges record |C(e)| / min id; U edges' parent minima (LDS-combined) + relabel
+        {
+            int32_t *skey = tab, *smin = tab + KS;
+            auto clear = [&]() {
+                for (int k = t; k < KS; k += TB) {
+                    skey[k] = -1;
+                    smin[k] = INT32_MAX;
+                }
+                if (t == 0) s_used = 0;
+            };
+            auto flush = [&]() {
+                for (int k = t; k < KS; k += TB) {
+                    const int32_t R = skey[k];
+                    if (R < 0) continue;
+                    if (((volatile int32_t *)c.parent)[R] > smin[k]) atomicMin(&c.parent[R], smin[k]);
+                }
+            };
+            clear();
+            __syncthreads();
+            for (int64_t base = i0; base < i1; base += TB) {
+                const int64_t i = base + t;
+                if (i < i1) {
+                    const int64_t r = l_rank(i, b);
+                    {
+                        const int32_t rep = c.hooked[r];
+                        const LRec q = c.lr[rep];
+                        if (q.rootedge == (int32_t)r) {
+                            c.esize[r] = q.csize + (rep < c.n ? 1 : c.esize[rep - c.n]);
+                            c.eminid[r] = min(q.cmin, rep < c.n ? vid(c, rep) : c.eminid[rep - c.n]);
+                        }
+                    }
+                    const int64_t u = r | half;
+                    if (u < c.m) {
+#pragma unroll
+                        for (int s = 0; s < 2; s++) {
+                            const int32_t x = c.lab[2 * u + s];
+                            if (c.stamp[x] == 2 * j) {
+                                const int32_t R = c.lr[uf_find(c.lr, x)].rootedge;
+                                uint32_t h = uf_prio(R, 0) & (KS - 1);
+                                while (true) {
+                                    const int32_t k = atomicCAS(&skey[h], -1, R);
+                                    if (k == -1) {
+                                        atomicAdd(&s_used, 1);
+                                        break;
+                                    }
+                                    if (k == R) break;
+                                    h = (h + 1) & (KS - 1);
+                                }
+                                atomicMin(&smin[h], (int32_t)u);
+                                c.lab[2 * u + s] = (int32_t)(c.n + R);
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+                if (base + TB < i1 && s_used > KS / 2 - 2 * TB) {
+                    flush();
+                    __syncthreads();
+                    clear();
+                    __syncthreads();
+                }
+            }
+            flush();
+        }
+        dc_phase_sync();
+    }
+    if (e_cyc) atomicOr(err, FE_CYCLE);
+}
+
 // Deep depths in one launch, in parallel: a workgroup takes a block of 2^LB consecutive ranks
 // whose labels name the components of F_{<lo} and runs the same rank divide and conquer on
 // LDS (labels hashed to local ids, contracted labels = HS + local root-edge rank, an LDS
@@ -1512,7 +1684,9 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     while ((int64_t(1) << J) <= m) J++;  // 2^J > m: every rank < m has a clear bit below J
     // global depths split blocks down to 2^LB ranks; dc_block (dc_local) finishes each such block
     const int LB = ctx->flat_block_log >= 8 && ctx->flat_block_log <= 10 ? ctx->flat_block_log : LOC_LOG;
-    for (int j = 0; j < J - LB; j++) {
+    // depths LM-1 .. LB per workgroup (dc_mid), the shallower ones global
+    const int LM = ctx->flat_mid_log > LB ? std::max(LB, std::min(ctx->flat_mid_log, J)) : LB;
+    for (int j = 0; j < J - LM; j++) {
         const int b = J - 1 - j;
         // L ranks (bit b clear) below m; every U rank is an L rank + 2^b
         const int64_t blk = int64_t(1) << (b + 1), half = int64_t(1) << b;
@@ -1537,6 +1711,9 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
         else
             hipLaunchKernelGGL(dc_link, dim3(gl), dim3(256), 0, st, dc, b, j, nl);
     }
+    if (LM > LB)
+        hipLaunchKernelGGL(dc_mid<1024>, dim3((unsigned)ceil_div(m, int64_t(1) << LM)), dim3(1024), 0, st, dc, J, LM, LB,
+                           err);
     const unsigned nblk = (unsigned)std::min<int64_t>(ceil_div(m, int64_t(1) << LB), 65536);
     switch (ctx->flat_block_log) {
     case 8: hipLaunchKernelGGL((dc_block<8, 128>), dim3(nblk), dim3(128), 0, st, dc, err); break;

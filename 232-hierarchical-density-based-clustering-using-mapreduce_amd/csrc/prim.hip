@@ -21,7 +21,17 @@
 
 #include "internal.hpp"
 
+// The speculative cooperative Prim (prim_coop_slots 6, round 5) is built only with
+// -DHDB_PRIM_SPEC=1 (HDBMI_EXTRA_FLAGS): exact and faster alone (1.91 vs 2.07 us/step at
+// 16,384 x 8) but slower inside the C5 job, where several Prims share the device (DESIGN §4
+// "Round 5" item 3), so the default library leaves it out; slots 6 then reports HDB_EUNSUPPORTED.
+#ifndef HDB_PRIM_SPEC
+#define HDB_PRIM_SPEC 0
+#endif
+
 namespace hdb {
+
+bool hdb_prim_spec_built() { return HDB_PRIM_SPEC != 0; }
 
 // exact mrd for (cur, nb); returns true if it improves best
 __device__ __forceinline__ bool mrd_improves(const PrimIn &in, int64_t cur, int64_t nb, double best, double &mrd_out) {
@@ -1227,6 +1237,7 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
     }
 }
 
+#if HDB_PRIM_SPEC
 // ------------------------------------------ cooperative kernel, speculative steps (slots 6)
 // The same Prim (HDBSCANStar.java:124-205 / HdbscanDataBubbles.java:165-254: select the
 // unattached vertex with the smallest best, ties -> largest index; update iff mrd < best,
@@ -1848,6 +1859,7 @@ static bool launch_spec(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, in
     HDB_THROW(HDB_EDEVICE, "prim_spec: exchange timed out (workgroups not co-resident)");
     return true;
 }
+#endif  // HDB_PRIM_SPEC
 
 template <int DM, bool FAST>
 static bool launch_coop2(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
@@ -1980,11 +1992,13 @@ void prim_batched_device(hdb_ctx *ctx, const PrimIn &in, const int64_t *h_offs, 
             int64_t n = h_offs[p + 1] - h_offs[p];
             const int64_t o = h_offs[p] - h_offs[0];
             bool ok = false;
+#if HDB_PRIM_SPEC
             if (n <= 65536 && ctx->prim_coop_slots == 6) {  // speculative steps, one exchange per round
                 if (in.d <= 4) ok = launch_spec<4>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
                 else if (in.d <= 8) ok = launch_spec<8>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
                 else if (in.d <= 16) ok = launch_spec<16>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
             }
+#endif
             if (n <= 65536 && ctx->prim_coop_slots == 4) {  // DPP folds + key/row granules
                 if (in.d <= 4) ok = launch_coop4<4, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
                 else if (in.d <= 8) ok = launch_coop4<8, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);

@@ -444,7 +444,8 @@ def predicted_scaling(drv, par, ns=(1, 2, 4, 8)):
             tot["nearest_sample"] += ph.get("nearest_sample", 0.0) / N
             # D11: the slice partials shard over the ranks (a rank folds its slices); the merge
             # of the gathered partials and the host copy of rep / info do not
-            tot["bubbles"] += ph.get("bubble_partials", 0.0) / min(N, drv.bubble_slices) + ph.get("bubbles", 0.0)
+            tot["bubbles"] += (ph.get("bubble_partials", 0.0) / min(N, getattr(drv, "bubble_slices", 1))
+                               + ph.get("bubbles", 0.0))
         per[N] = {k: round(v, 3) for k, v in tot.items()} | {"fixed": round(fixed, 3)}
         out[N] = sum(tot.values()) + fixed
     return {"model": "LPT makespan of the measured N=1 task durations per level (local models; leaves "

@@ -572,6 +572,8 @@ def test_prim_cooperative_vs_oracle(pkg, oracle, n, kind):
     ctx = pkg.Context.get(0)
     star = pkg.HDBSCANStar(ctx)
     for coop, slots in ((1, 6), (1, 5), (1, 4), (1, 3), (1, 2), (1, 1), (1, 0), (0, 0)):
+        if not _slots_built(pkg, slots):
+            continue
         ctx.set_option("prim_coop", coop)
         ctx.set_option("prim_coop_slots", slots)
         try:
@@ -593,6 +595,8 @@ def test_prim_coop_plain_timeout_retries_cooperatively(pkg, oracle):
     star = pkg.HDBSCANStar(ctx)
     before = ctx.get_stat("prim_coop_plain_retries")
     for slots in (4, 5, 6):
+        if not _slots_built(pkg, slots):
+            continue
         ctx.set_option("prim_coop_slots", slots)
         ctx.set_option("prim_coop_plain_spin_log2", 0)
         try:
@@ -612,11 +616,29 @@ def test_prim_coop_slots_metrics_and_bubbles(pkg, oracle, d, metric, n, slots):
     speculative one (slots 6: many steps per exchange, undone past the first wrong pick) equal
     the reference Prim for every metric, and the bubble Prim (HdbscanDataBubbles.java:165-254,
     the C3/C5 bubble models they were written for) on > 4096 bubbles, up to 64 workgroups."""
+    _need_slots(pkg, slots)
     pkg.Context.get(0).set_option("prim_coop_slots", slots)
     try:
         _coop_slots_case(pkg, oracle, d, metric, n)
     finally:
         pkg.Context.get(0).set_option("prim_coop_slots", 4)
+
+
+def _slots_built(pkg, slots):
+    """slots 6 (the speculative Prim) exists only in a -DHDB_PRIM_SPEC=1 build"""
+    c = pkg.Context.get(0)
+    try:
+        c.set_option("prim_coop_slots", slots)
+    except pkg.HdbError:
+        return False
+    finally:
+        c.set_option("prim_coop_slots", 4)
+    return True
+
+
+def _need_slots(pkg, slots):
+    if not _slots_built(pkg, slots):
+        pytest.skip("speculative Prim not built (HDBMI_EXTRA_FLAGS=-DHDB_PRIM_SPEC=1)")
 
 
 def _coop_slots_case(pkg, oracle, d, metric, n):
