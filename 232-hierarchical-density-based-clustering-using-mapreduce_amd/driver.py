@@ -71,7 +71,8 @@ class MRHDBSCANStar:
     def __init__(self, minPts=4, minClSize=4, processing_units=50, k=0.2, samples_per_subset=None,
                  seed=20210101, distanceFunction=None, all_inter_edges=True, max_levels=64, ctx=None,
                  device=0, flat_labels=True, profile=False, exact_prim_leaves=False, group=None,
-                 prim_leaf_max=LEAF_PRIM_MAX, model_threads=4, defer_leaves=True, bubble_slices=BUBBLE_SLICES):
+                 prim_leaf_max=LEAF_PRIM_MAX, model_threads=4, defer_leaves=True, bubble_slices=BUBBLE_SLICES,
+                 emulate_ranks=()):
         self.minPts = minPts
         self.minClSize = minClSize
         self.processing_units = processing_units
@@ -109,6 +110,14 @@ class MRHDBSCANStar:
         self.bubble_slices = int(bubble_slices)
         if not 1 <= self.bubble_slices <= 64:
             raise ValueError("bubble_slices: 1..64")
+        # profile at N = 1 only: after every level's local models (and the deferred leaves) ran
+        # for real, run them again once per N in emulate_ranks as the N-rank driver would --
+        # each rank's LPT share on its own, one rank after another -- and record the slowest
+        # rank's wall time (bench.py predicted_scaling).  A rank then gets the concurrency its
+        # own share allows, not the one-device pool's: with ~8 models per level, 8 ranks hold
+        # one or two each, and a lone model runs at its own (latency-bound) speed.
+        self.emulate_ranks = tuple(int(x) for x in emulate_ranks)
+        self._emulating = False
         self._pool = None
         self.group = group      # torch.distributed group (None: the default group, if any)
         self._comm = None       # HdbComm for the merge under nccl
@@ -141,7 +150,7 @@ class MRHDBSCANStar:
     def _task(self, kind, weight, seconds):
         """profile: one task's duration in the current level (the LPT weight the sharded
         driver assigns it by, and its measured seconds at this world size)"""
-        if self.profile and self._lvl is not None:
+        if self.profile and self._lvl is not None and not self._emulating:
             self._lvl.setdefault(kind, []).append((float(weight), float(seconds)))
 
     # ------------------------------------------------------------------ helpers
@@ -388,6 +397,9 @@ class MRHDBSCANStar:
                 results = dict(zip(mine, self._pool.map(model, mine)))
             else:
                 results = {i: model(i) for i in mine}
+            if self.profile and self.emulate_ranks and world == 1:
+                self._lvl["emulated_local_models"] = self._emulate(
+                    [int(ne.shape[0]) ** 2 for ne in nonempty_of], lambda grp: self._run_group(model_body, grp))
             if world > 1:
                 for part in P.allgather_object(results, self.group):
                     results.update(part)
@@ -438,6 +450,10 @@ class MRHDBSCANStar:
                 blocks.extend((pending[j][0], e) for j, e in zip(mine, got))
             if self.profile:
                 self._lvl["phase_s"]["leaves"] = self._mark("leaves")
+            if self.profile and self.emulate_ranks and world == 1:
+                self._lvl["emulated_leaves"] = self._emulate(
+                    [int(r.shape[0]) ** 2 for _, r in pending],
+                    lambda grp: self._leaves(X, [pending[j][1] for j in grp], list(range(len(grp)))))
         # UnionFindReducer + SortMST: stable descending sort of the iteration-major
         # concatenation (leaf blocks in key order, then the level's inter-cluster blocks)
         order = sorted(block_size)
@@ -472,6 +488,44 @@ class MRHDBSCANStar:
             out["labels"] = labels
             out["n_clusters"] = int(k[0])
             self._mark("flat_labels")
+        return out
+
+    def _run_group(self, fn, grp):
+        """run fn over the items of one (emulated) rank as the model pool would"""
+        if len(grp) > 1 and self.model_threads > 1:
+            if self._pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+                self._pool = ThreadPoolExecutor(self.model_threads)
+            return list(self._pool.map(fn, grp))
+        return [fn(i) for i in grp]
+
+    def _emulate(self, costs, run):
+        """profile: {N: wall time of the slowest rank} with the items dealt by the driver's LPT
+        to N ranks, every rank's share run alone (synchronised), one rank after another"""
+        import time
+        import torch
+        out = {}
+        torch.cuda.synchronize(self.device)
+        t_in = time.perf_counter()
+        self._emulating = True
+        try:
+            for N in self.emulate_ranks:
+                own = P.lpt(costs, N)
+                worst = 0.0
+                for r in range(N):
+                    grp = [i for i in range(len(costs)) if own[i] == r]
+                    if not grp:
+                        continue
+                    torch.cuda.synchronize(self.device)
+                    t0 = time.perf_counter()
+                    run(grp)
+                    torch.cuda.synchronize(self.device)
+                    worst = max(worst, time.perf_counter() - t0)
+                out[N] = worst
+        finally:
+            self._emulating = False
+        if self._t0 is not None:  # the phase being measured does not include the emulation
+            self._t0 += time.perf_counter() - t_in
         return out
 
     def _bubbles_sliced(self, c, Xb, nearest, nb, world, rank, ls, ss, rep, info):

@@ -424,23 +424,28 @@ def predicted_scaling(drv, par, ns=(1, 2, 4, 8)):
     batch after the level loop) are one more "level" holding only leaves, so their LPT runs
     over the whole job.  Not modelled: the all-gathers and the RCCL merge exchange."""
     fixed = sum(v for k, v in drv.timings.items() if k in ("bookkeeping", "merge", "flat_labels"))
-    out, per = {}, {}
+    out, per, lpt_model = {}, {}, {}
     for N in ns:
         tot = {"leaves": 0.0, "local_models": 0.0, "nearest_sample": 0.0, "bubbles": 0.0}
+        lpt_tot = 0.0  # round 3-5's estimate, kept beside: N = 1 task times x the one-device concurrency
         for L in drv.level_tasks:
             ph = L["phase_s"]
             for kind in ("leaves", "local_models"):
                 tasks = L.get(kind, [])
                 wall = ph.get(kind, 0.0)
                 work = sum(t for _, t in tasks)
+                em = L.get("emulated_" + kind, {})
                 if not tasks or work <= 0:
-                    tot[kind] += wall
-                    continue
-                owner = par.lpt([w for w, _ in tasks], N)
-                load = np.zeros(N)
-                for (w, t), o in zip(tasks, owner):
-                    load[o] += t
-                tot[kind] += float(load.max()) * wall / work
+                    est = wall
+                else:
+                    owner = par.lpt([w for w, _ in tasks], N)
+                    load = np.zeros(N)
+                    for (w, t), o in zip(tasks, owner):
+                        load[o] += t
+                    est = float(load.max()) * wall / work
+                lpt_tot += est
+                # emulated: every rank's LPT share run on its own (driver emulate_ranks)
+                tot[kind] += wall if N == 1 else em.get(N, est)
             tot["nearest_sample"] += ph.get("nearest_sample", 0.0) / N
             # D11: the slice partials shard over the ranks (a rank folds its slices); the merge
             # of the gathered partials and the host copy of rep / info do not
@@ -448,14 +453,22 @@ def predicted_scaling(drv, par, ns=(1, 2, 4, 8)):
                                + ph.get("bubbles", 0.0))
         per[N] = {k: round(v, 3) for k, v in tot.items()} | {"fixed": round(fixed, 3)}
         out[N] = sum(tot.values()) + fixed
-    return {"model": "LPT makespan of the measured N=1 task durations per level (local models; leaves "
-                     "deferred: one LPT over the whole job), "
+        lpt_model[N] = out[N] - tot["leaves"] - tot["local_models"] + lpt_tot
+    emulated = any("emulated_local_models" in L for L in drv.level_tasks)
+    return {"model": ("local models and leaves EMULATED per level: each of the N ranks' LPT share run on its "
+                      "own on this GPU, the slowest rank counted (driver emulate_ranks); " if emulated else
+                      "LPT makespan of the measured N=1 task durations x the one-device concurrency per level; ") +
                      "nearest sample / N, bubble slice partials / min(N, slices), their merge + "
                      "bookkeeping + merge + flat labels unscaled; "
                      "all-gathers and the RCCL merge exchange not modelled",
             "seconds": {str(N): round(v, 3) for N, v in out.items()},
             "speedup": {str(N): round(out[1] / v, 2) for N, v in out.items()},
-            "phases": {str(N): v for N, v in per.items()}}
+            "phases": {str(N): v for N, v in per.items()},
+            "lpt_concurrency_estimate": {"speedup": {str(N): round(out[1] / v, 2) for N, v in lpt_model.items()},
+                                         "note": "rounds 3-5's model: N = 1 task durations (measured while the "
+                                                 "model pool shares the GPU) x that level's one-device concurrency "
+                                                 "factor -- optimistic when a rank holds one or two models, which "
+                                                 "then run at their own latency-bound speed"}}
 
 
 def run_partitioned(args, workload):
@@ -481,7 +494,8 @@ def run_partitioned(args, workload):
     X_pin = torch.from_numpy(C[rng.integers(0, cfg["centers"], size=n)] +
                              rng.normal(0, 1.0, size=(n, cfg["d"]))).pin_memory()
     drv = pkg.MRHDBSCANStar(minPts=MIN_PTS, minClSize=MIN_CL_SIZE, processing_units=cfg["processing_units"],
-                            samples_per_subset=cfg["samples_per_subset"], profile=args.phases)
+                            samples_per_subset=cfg["samples_per_subset"], profile=args.phases,
+                            emulate_ranks=(2, 4, 8) if args.phases and world == 1 else ())
     out = {}
 
     if os.environ.get("HDB_WATCHDOG"):  # diagnosis: every thread's Python stack every N s
