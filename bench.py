@@ -167,10 +167,10 @@ MFMA_BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
 # HBM bytes per launch from the PMC passes of this build (FETCH_SIZE / WRITE_SIZE runs of their
 # own, corrected by tools/pmc_summary.py): tools/profile_bench.sh (C2), tools/profile_c4.sh (C4)
 PMC_C2 = next((p for p in (os.path.join(ROOT, "profiles", r, "final", "prof_c2", "pmc_summary.json")
-                            for r in ("r05", "r04", "r03", "r02")) if os.path.exists(p)),
+                            for r in ("r06", "r05", "r04", "r03", "r02")) if os.path.exists(p)),
               os.path.join(ROOT, "profiles", "r02", "final", "prof_c2", "pmc_summary.json"))
 PMC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, "c4_final", "pmc_summary.json")
-                            for r in ("r05", "r04", "r03", "r02")) if os.path.exists(p)),
+                            for r in ("r06", "r05", "r04", "r03", "r02")) if os.path.exists(p)),
               os.path.join(ROOT, "profiles", "r02", "c4_final", "pmc_summary.json"))
 
 
@@ -494,8 +494,7 @@ def run_partitioned(args, workload):
     X_pin = torch.from_numpy(C[rng.integers(0, cfg["centers"], size=n)] +
                              rng.normal(0, 1.0, size=(n, cfg["d"]))).pin_memory()
     drv = pkg.MRHDBSCANStar(minPts=MIN_PTS, minClSize=MIN_CL_SIZE, processing_units=cfg["processing_units"],
-                            samples_per_subset=cfg["samples_per_subset"], profile=args.phases,
-                            emulate_ranks=(2, 4, 8) if args.phases and world == 1 else ())
+                            samples_per_subset=cfg["samples_per_subset"], profile=args.phases)
     out = {}
 
     if os.environ.get("HDB_WATCHDOG"):  # diagnosis: every thread's Python stack every N s
@@ -560,6 +559,13 @@ def run_partitioned(args, workload):
     barrier()
     for c in list(A.Context._all):
         c.set_option("count_evals", 0)
+    if args.phases and world == 1:
+        # one more untimed job for predicted_scaling: the real phases plus every level's local
+        # models and the deferred leaves re-run as 2, 4 and 8 ranks would run them (emulate_ranks)
+        drv.emulate_ranks = (2, 4, 8)
+        job()
+        barrier()
+        drv.emulate_ranks = ()
     k2b_roof = boruvka_roofline(kt.get("boruvka_scan", [0.0, 0])[0] / args.steps,
                                 (stat_total("boruvka_bound_ns_sum") - b0["boruvka_bound_ns_sum"]) * 1e-9,
                                 stat_total("boruvka_evals_sum") - b0["boruvka_evals_sum"], cfg["d"])
