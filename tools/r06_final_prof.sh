@@ -5,8 +5,7 @@
 # line's roofline.traffic reads the summary of the same build.
 # Usage (repo root, on the box): bash tools/r06_final_prof.sh <outdir>
 set -uo pipefail
-OUT=$(readlink -f "${1:?outdir}")
-mkdir -p "$OUT"; export TMPDIR=/tmp
+mkdir -p "${1:?outdir}"; OUT=$(readlink -f "$1"); export TMPDIR=/tmp
 export GPU_MAX_HW_QUEUES=8  # as bench.py sets it (the profiler initialises HIP before bench.py runs)
 timeout -k 10 700 bash tools/profile_bench.sh "$OUT/prof_c2" > "$OUT/prof_c2.log" 2>&1 || { echo "c2 profile failed"; tail "$OUT/prof_c2.log"; exit 1; }
 timeout -k 10 600 bash tools/c4prof.sh "$OUT/c4_prof" > "$OUT/c4_prof.log" 2>&1 || { echo "c4 profile failed"; tail "$OUT/c4_prof.log"; exit 1; }
