@@ -6,7 +6,7 @@ In production the Java/Spark driver stays in place and calls the operators throu
 stay in HBM for the whole run, every level's work is batched over all subsets of the level,
 and only per-subset bookkeeping (a few integers per subset, one label per bubble) touches
 the host.  Semantics follow Main.java with the deterministic deviations of SURVEY.md
-Appendix A.2 (D1-D10, listed in oracle/mr_driver.py, which restates the same loop on the CPU
+Appendix A.2 (D1-D11, listed in oracle/mr_driver.py, which restates the same loop on the CPU
 oracle for the parity tests):
 
   level loop (Main.java:107)   subsets grouped by key, ascending (D5)
@@ -19,15 +19,16 @@ oracle for the parity tests):
           the subset tree, so they are deferred (defer_leaves): every level's leaves run as
           one batch after the level loop (identical blocks, placed by their canonical ids)
   big subsets: D2 samples -> keyed nearest sample (FirstStep.java:74-85, D3) -> bulk
-          CombineStep (D5 fold order) -> per subset LocalModelReduceByKey (D4) -> partition
+          CombineStep (D5 fold order per slice, D11 merge) -> per subset LocalModelReduceByKey (D4) -> partition
           induction (Main.java:272-289, including the in-place relabel) -> LabelClassification
   merge   UnionFindReducer + SortMST: stable descending sort of the iteration-major edge list
 
 Multi-GPU (one process per GPU, torch.distributed initialised, X given to
 every rank): the plan is computed identically on every rank -- leaves go to ranks by LPT on
 n_i^2 (over the whole job when deferred, per level otherwise), the big subsets' points are split in contiguous chunks for the nearest-sample scan (the
-assignments are all-gathered), bubble statistics are recomputed on every rank (the D5 fold
-order keeps them bit-exact), local models go to ranks by LPT on b_i^2 (results all-gathered
+assignments are all-gathered), bubble statistics are folded per fixed row slice by the rank
+that owns the slice and the gathered partials merged in slice order (D11: the same result at
+every rank count), local models go to ranks by LPT on b_i^2 (results all-gathered
 and applied in subset order), and the merge places every local edge at its position in the
 single-device concatenation (hdb_merge_edges over the library's RCCL communicator under
 nccl, torch.distributed under gloo) before the stable sort.  Every rank returns the same
