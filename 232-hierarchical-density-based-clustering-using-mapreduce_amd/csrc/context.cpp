@@ -405,7 +405,7 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
         return HDB_OK;
     }
     if (k == "prim_coop_slots") {
-        if (value < 0 || value > 7) return HDB_EINVAL;
+        if (value < 0 || value > 6) return HDB_EINVAL;
         if (value == 6 && !hdb_prim_spec_built()) {  // csrc/prim.hip: only with -DHDB_PRIM_SPEC=1
             set_error("prim_coop_slots 6: the speculative Prim is not in this build (-DHDB_PRIM_SPEC=1)");
             return HDB_EUNSUPPORTED;

@@ -1237,314 +1237,6 @@ static bool launch_coop4(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, i
     }
 }
 
-// Variant (prim_coop_slots = 7, round 6): every WAVE publishes its own candidate, no workgroup
-// fold.  The slots-4 step spends ~1,800 of its ~5,600 cycles between the waves' minima and the
-// publish (the winner lane parks its row in LDS, a workgroup barrier, wave 0 folds the 16 waves
-// and reads the winner's row back: tools/coop_prof.py, profiles/r04/prim/coopprof*.log).  Here a
-// wave's minimum lane hands its key and row to the publishing lanes with readlane (scalar, no
-// LDS) and the wave stores its 3 key + 2 (DM + 3) row granules itself; wave 0 of every workgroup
-// sweeps the key granules of all nwg x NW waves (entries in index order, so the select rule --
-// smallest key, ties to the largest index -- is "ties to the last entry"), reads the winner
-// wave's row granules into LDS, and ONE barrier per step remains.  A wave's candidate is cached
-// as in slots 4 (republished under the new tag when none of its lanes improved or was attached).
-// Double buffering by step parity is safe for the same reason: a wave publishes step t + 1 only
-// after its workgroup's sweep of step t, which needed every wave's step-t granules, each
-// published after its own workgroup finished sweeping step t - 1.
-template <int BS, int DM>
-__global__ __launch_bounds__(BS) void prim_coop7_kernel(PrimIn in, int n, int self_edges, int32_t *__restrict__ va,
-                                                        int32_t *__restrict__ vb, double *__restrict__ w,
-                                                        gu64 *__restrict__ gkey, gu64 *__restrict__ grow, int *err,
-                                                        unsigned spin_limit, int spread, int *__restrict__ xcc,
-                                                        int res) {
-    if ((int)(blockIdx.x % spread) != res) return;  // an idle block of a spread grid
-    constexpr int NW = BS / 64;
-    constexpr int ND = DM + 3;  // x, core, eB, nnB
-    constexpr int MAXE = 64 * NW;  // entries (waves) of a grid of <= 64 workgroups
-    __shared__ unsigned s_key[3 * MAXE];
-    __shared__ double s_row[ND];
-    __shared__ int s_cur, s_local;
-    const int nwg = (int)gridDim.x / spread;
-    const int bid = (int)blockIdx.x / spread;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int i = bid * BS + tid;
-    const int E = nwg * NW;          // published entries per step
-    const int ent = bid * NW + wid;  // this wave's entry (index order)
-    if (tid == 0) s_local = 0;
-    if (spread > 1 && wid == 0) {  // every working block on one XCC?
-        if (lane == 0) {
-            unsigned x;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-            __hip_atomic_store(xcc + bid, (int)(x & 15u) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        bool same = true;
-        int first = 0;
-        for (unsigned spins = 0;;) {
-            bool ok = true;
-            int mn = 1 << 30, mx = -1;
-            for (int j = lane; j < nwg; j += 64) {
-                const int v = __hip_atomic_load(xcc + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok &= v != 0;
-                mn = min(mn, v);
-                mx = max(mx, v);
-            }
-            if (__all(ok)) {
-                for (int o = 32; o >= 1; o >>= 1) {
-                    mn = min(mn, __shfl_xor(mn, o));
-                    mx = max(mx, __shfl_xor(mx, o));
-                }
-                same = mn == mx;
-                first = mn;
-                break;
-            }
-            if (++spins > spin_limit) {  // not co-resident: the retry takes over
-                if (lane == 0) atomicExch(err, 1);
-                first = -1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (lane == 0) s_local = first < 0 ? -1 : (same && first > 0);
-    }
-    __syncthreads();
-    if (s_local < 0) return;
-    const bool local = s_local != 0;
-    double xi[DM], ci = 0, ebi = 0, nni = 0;
-#pragma unroll
-    for (int c = 0; c < DM; c++) xi[c] = (i < n && c < in.d) ? in.X[(int64_t)i * in.d + c] : 0.0;
-    if (i < n) {
-        ci = in.core[i];
-        if (in.eB) {
-            ebi = in.eB[i];
-            nni = in.nnB[i];
-        }
-    }
-    double best = JMAX;
-    int par = -1;
-    bool att = (i >= n) || (i == n - 1);
-    double xc[DM], cc, ebc = 0, nnc = 0;
-#pragma unroll
-    for (int c = 0; c < DM; c++) xc[c] = c < in.d ? in.X[(int64_t)(n - 1) * in.d + c] : 0.0;
-    cc = in.core[n - 1];
-    if (in.eB) {
-        ebc = in.eB[n - 1];
-        nnc = in.nnB[n - 1];
-    }
-    int cur = n - 1;
-    constexpr unsigned long long KINF = 0x7ff0000000000000ull;  // key of +inf: nothing to offer
-    bool just = false;    // this lane was attached at the end of the last step
-    unsigned val_c = 0u;  // this lane's cached granule value (the wave's candidate)
-    const int P = (E + 63) / 64;  // entries per sweeping lane (contiguous: index order kept)
-    for (int step = 1; step < n; step++) {
-        bool imp = false;
-        double mrd = 0.0;
-        if (!att) mrd = coop_mrd<DM>(in, xc, cc, ebc, nnc, xi, ci, ebi, nni, best, imp);
-        if (imp) {
-            best = mrd;
-            par = cur;
-        }
-        const bool dirty = step == 1 || __any(imp || just);
-        just = false;
-        if (dirty) {
-            const unsigned long long key = att ? KINF : mrd_key(best);
-            const unsigned long long wmin = wave_min_u64(key);
-            const int wl = last_lane(key == wmin);  // wave-uniform
-            // lanes 0-2: value lo, value hi, index; lanes 3 .. 2 ND + 2: the row's halves
-            unsigned v = 0u;
-            {
-                const unsigned long long bb = (unsigned long long)__double_as_longlong(best);
-                const unsigned lo = __builtin_amdgcn_readlane((unsigned)bb, wl);
-                const unsigned hi = __builtin_amdgcn_readlane((unsigned)(bb >> 32), wl);
-                const int idx = wmin < KINF ? bid * BS + wid * 64 + wl : -1;
-                v = lane == 0 ? lo : (lane == 1 ? hi : (unsigned)idx);
-            }
-#pragma unroll
-            for (int c = 0; c < ND; c++) {
-                const double x = c < DM ? xi[c < DM ? c : 0] : (c == DM ? ci : (c == DM + 1 ? ebi : nni));
-                const unsigned long long xb = (unsigned long long)__double_as_longlong(x);
-                const unsigned lo = __builtin_amdgcn_readlane((unsigned)xb, wl);
-                const unsigned hi = __builtin_amdgcn_readlane((unsigned)(xb >> 32), wl);
-                if (lane == 3 + 2 * c) v = lo;
-                if (lane == 4 + 2 * c) v = hi;
-            }
-            val_c = v;
-        }
-        const int buf = step & 1;
-        const unsigned tag = (unsigned)step;
-        {
-            const unsigned long long gv = ((unsigned long long)tag << 32) | val_c;
-            gu64 *dst = nullptr;
-            if (lane < 3)
-                dst = gkey + ((size_t)buf * E + ent) * 3 + lane;
-            else if (lane < 3 + 2 * ND)
-                dst = grow + ((size_t)buf * E + ent) * (2 * ND) + (lane - 3);
-            if (dst) {  // plain stores when every working block shares one XCD (see slots 4)
-                if (local)
-                    __hip_atomic_store(dst, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                else
-                    __hip_atomic_store(dst, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        if (wid == 0) {
-            const gu64 *kb = gkey + (size_t)buf * E * 3;
-            const int T = 3 * E;
-            bool tmo = false;
-            for (unsigned spins = 0;;) {
-                bool ok = true;
-                for (int j = lane; j < T; j += 64) {
-                    const unsigned long long x = __hip_atomic_load(kb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok &= (unsigned)(x >> 32) == tag;
-                    s_key[j] = (unsigned)x;
-                }
-                if (__all(ok)) break;
-                if (++spins > spin_limit) {  // a co-residency failure must not hang the device
-                    if (lane == 0) atomicExch(err, 1);
-                    tmo = true;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            __builtin_amdgcn_wave_barrier();
-            // lane L: entries [L P, L P + P); ties go to the later entry, then to the later lane
-            unsigned long long lk = KINF;
-            int le = -1, lidx = -1;
-            for (int q = 0; q < P; q++) {
-                const int e = lane * P + q;
-                if (e >= E) break;
-                const int kidx = (int)s_key[3 * e + 2];
-                if (kidx < 0) continue;
-                const double kv = __longlong_as_double((long long)(((unsigned long long)s_key[3 * e + 1] << 32) | s_key[3 * e]));
-                const unsigned long long kk = mrd_key(kv);
-                if (kk <= lk) {
-                    lk = kk;
-                    le = e;
-                    lidx = kidx;
-                }
-            }
-            const unsigned long long amin = wave_min_u64(lk);
-            const int k = last_lane(lk == amin);
-            const int wen = __builtin_amdgcn_readlane(le, k);
-            const int win = __builtin_amdgcn_readlane(lidx, k);
-            if (tmo || amin == KINF || wen < 0) {
-                if (lane == 0) s_cur = -1;
-            } else {
-                bool row_tmo = false;
-                if (lane < 2 * ND) {  // the winner wave's row granules, straight into the LDS row
-                    const gu64 *rb = grow + ((size_t)buf * E + wen) * (2 * ND) + lane;
-                    unsigned long long x;
-                    for (unsigned spins = 0;;) {
-                        x = __hip_atomic_load(rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if ((unsigned)(x >> 32) == tag) break;
-                        if (++spins > spin_limit) {  // a stale row must not be used: report, exit
-                            row_tmo = true;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                    ((unsigned *)s_row)[lane] = (unsigned)x;
-                }
-                if (__any(row_tmo)) {
-                    if (lane == 0) {
-                        atomicExch(err, 1);
-                        s_cur = -1;
-                    }
-                } else if (lane == 0)
-                    s_cur = win;
-            }
-        }
-        __syncthreads();
-        cur = s_cur;
-        if (cur < 0) break;
-#pragma unroll
-        for (int c = 0; c < DM; c++) xc[c] = s_row[c];
-        cc = s_row[DM];
-        ebc = s_row[DM + 1];
-        nnc = s_row[DM + 2];
-        if (i == cur) {
-            att = true;
-            just = true;
-        }
-        // no barrier needed before the next step's LDS writes: s_row / s_cur are written again
-        // only after the next sweep, which waits for every wave's next publish -- issued after
-        // that wave read them here
-    }
-    if (i < n - 1) {
-        va[i] = par >= 0 ? in.ids[par] : 0;
-        vb[i] = in.ids[i];
-        w[i] = best;
-    }
-    if (self_edges && i < n) {
-        va[n - 1 + i] = in.ids[i];
-        vb[n - 1 + i] = in.ids[i];
-        w[n - 1 + i] = in.core[i];
-    }
-}
-
-template <int DM>
-static bool launch_coop7(hdb_ctx *ctx, const PrimIn &in, int64_t o, int64_t n, int64_t eo, int self_edges,
-                         int32_t *va, int32_t *vb, double *w) {
-    constexpr int BS = 1024, NW = BS / 64;
-    const int nwg = (int)ceil_div(n, BS);
-    if (nwg > 64) return false;
-    int coop = 0, ncu = 0, per_cu = 0;
-    HIP_CHECK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device));
-    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, prim_coop7_kernel<BS, DM>, BS, 0));
-    if (!coop || (int64_t)per_cu * ncu < nwg) return false;
-    constexpr int ND = DM + 3;
-    const int E = nwg * NW;
-    const size_t kbytes = (8 * (size_t)3 * 2 * E + 255) & ~size_t(255);
-    const size_t rbytes = (8 * (size_t)2 * ND * 2 * E + 255) & ~size_t(255);
-    char *base = (char *)arena(ctx, A_WORK3, kbytes + rbytes + 512);
-    gu64 *gkey = (gu64 *)base;
-    gu64 *grow = (gu64 *)(base + kbytes);
-    int *err = (int *)(base + kbytes + rbytes);
-    int *xcc = err + 64;
-    HIP_CHECK(hipMemsetAsync(base, 0, kbytes + rbytes + 512, ctx->stream));  // tags 0: no step yet
-    PrimIn L = in;
-    L.X = in.X + o * in.d;
-    L.core = in.core + o;
-    L.ids = in.ids + o;
-    if (in.eB) {
-        L.eB = in.eB + o;
-        L.nnB = in.nnB + o;
-    }
-    int nn = (int)n;
-    int32_t *pva = va + eo, *pvb = vb + eo;
-    double *pw = w + eo;
-    unsigned spin = 1u << 24;
-    int spread1 = 1, res0 = 0;
-    void *args[] = {&L, &nn, &self_edges, &pva, &pvb, &pw, &gkey, &grow, &err, &spin, &spread1, &xcc, &res0};
-    const int spread = (ctx->prim_coop_xcd && nwg <= ctx->prim_coop_xcd_max_wg && nwg <= 32 * per_cu) ? 8 : 1;
-    static std::atomic<int> launches{0};  // rotates the XCD of concurrent Prims (a hint only)
-    const int res = spread > 1 ? (launches.fetch_add(1) & 7) : 0;
-    const unsigned plain_spin = 1u << ctx->prim_coop_plain_spin_log2;
-    int h_err = 0;
-    for (int attempt = ctx->prim_coop_plain ? 0 : 1; attempt < 2; attempt++) {
-        if (attempt == 1 && h_err) HIP_CHECK(hipMemsetAsync(base, 0, kbytes + rbytes + 512, ctx->stream));
-        {
-            KernelTimer t(ctx, "prim_coop");
-            if (attempt == 0)
-                hipLaunchKernelGGL((prim_coop7_kernel<BS, DM>), dim3(nwg * spread), dim3(BS), 0, ctx->stream, L, nn,
-                                   self_edges, pva, pvb, pw, gkey, grow, err, plain_spin, spread, xcc, res);
-            else
-                HIP_CHECK(hipLaunchCooperativeKernel((const void *)prim_coop7_kernel<BS, DM>, dim3(nwg), dim3(BS), args, 0,
-                                                     ctx->stream));
-            HIP_CHECK(hipGetLastError());
-        }
-        h_err = 0;
-        HIP_CHECK(hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-        HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        if (!h_err) {
-            ctx->stats["prim_coop_steps"] += n - 1;
-            ctx->stats["prim_coop_launches"] += 1;
-            return true;
-        }
-        if (attempt == 0) ctx->stats["prim_coop_plain_retries"] += 1;
-    }
-    HDB_THROW(HDB_EDEVICE, "prim_coop7: key sweep timed out (workgroups not co-resident)");
-    return true;
-}
-
 #if HDB_PRIM_SPEC
 // ------------------------------------------ cooperative kernel, speculative steps (slots 6)
 // The same Prim (HDBSCANStar.java:124-205 / HdbscanDataBubbles.java:165-254: select the
@@ -2311,11 +2003,6 @@ void prim_batched_device(hdb_ctx *ctx, const PrimIn &in, const int64_t *h_offs, 
                 if (in.d <= 4) ok = launch_coop4<4, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
                 else if (in.d <= 8) ok = launch_coop4<8, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
                 else if (in.d <= 16) ok = launch_coop4<16, false>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
-            }
-            if (n <= 65536 && ctx->prim_coop_slots == 7) {  // per-wave publish, no workgroup fold
-                if (in.d <= 4) ok = launch_coop7<4>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
-                else if (in.d <= 8) ok = launch_coop7<8>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
-                else if (in.d <= 16) ok = launch_coop7<16>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);
             }
             if (n <= 65536 && ctx->prim_coop_slots == 5) {  // ... every candidate row in the sweep
                 if (in.d <= 4) ok = launch_coop4<4, true>(ctx, in, o, n, eoff[p], self_edges, va, vb, w);

@@ -571,7 +571,7 @@ def test_prim_cooperative_vs_oracle(pkg, oracle, n, kind):
     va, vb, w = oracle.prim_mst(X, core)
     ctx = pkg.Context.get(0)
     star = pkg.HDBSCANStar(ctx)
-    for coop, slots in ((1, 7), (1, 6), (1, 5), (1, 4), (1, 3), (1, 2), (1, 1), (1, 0), (0, 0)):
+    for coop, slots in ((1, 6), (1, 5), (1, 4), (1, 3), (1, 2), (1, 1), (1, 0), (0, 0)):
         if not _slots_built(pkg, slots):
             continue
         ctx.set_option("prim_coop", coop)
@@ -594,7 +594,7 @@ def test_prim_coop_plain_timeout_retries_cooperatively(pkg, oracle):
     ctx = pkg.Context.get(0)
     star = pkg.HDBSCANStar(ctx)
     before = ctx.get_stat("prim_coop_plain_retries")
-    for slots in (4, 5, 6, 7):
+    for slots in (4, 5, 6):
         if not _slots_built(pkg, slots):
             continue
         ctx.set_option("prim_coop_slots", slots)
@@ -608,13 +608,12 @@ def test_prim_coop_plain_timeout_retries_cooperatively(pkg, oracle):
     assert ctx.get_stat("prim_coop_plain_retries") >= before + 1
 
 
-@pytest.mark.parametrize("slots", [4, 6, 7])
+@pytest.mark.parametrize("slots", [4, 6])
 @pytest.mark.parametrize("d,metric,n", [(8, "euclidean", 9000), (16, "euclidean", 5000), (5, "cosine", 6000),
                                         (2, "manhattan", 4500), (8, "euclidean", 16384), (3, "euclidean", 65536)])
 def test_prim_coop_slots_metrics_and_bubbles(pkg, oracle, d, metric, n, slots):
-    """The step-tagged cooperative Prim (rows in registers, d <= 16; slots 4), the per-wave
-    publishing one (slots 7) and the speculative one (slots 6: many steps per exchange, undone
-    past the first wrong pick) equal
+    """The step-tagged cooperative Prim (rows in registers, d <= 16; slots 4) and the
+    speculative one (slots 6: many steps per exchange, undone past the first wrong pick) equal
     the reference Prim for every metric, and the bubble Prim (HdbscanDataBubbles.java:165-254,
     the C3/C5 bubble models they were written for) on > 4096 bubbles, up to 64 workgroups."""
     _need_slots(pkg, slots)
