@@ -63,14 +63,24 @@ struct __align__(16) LRec {
     int32_t uf, rootedge, csize, cmin;
 };
 
+// Union-find words are read and written with relaxed agent-scope atomics (global_load / store
+// sc1: coherent in the L2, skip the CU's L1).  They were `volatile` until round 6, which on
+// gfx950 compiles to system-scope flat accesses (sc0 sc1) with a full vmcnt/lgkmcnt drain after
+// each -- every step of a find paid the system-scope round trip.
+__device__ __forceinline__ int32_t uf_ld(const int32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void uf_st(int32_t *p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ int32_t uf_find(LRec *lr, int32_t x) {
-    volatile int32_t *u = &lr->uf;  // stride 4 ints
+    int32_t *u = &lr->uf;  // stride 4 ints
     while (true) {
-        int32_t p = u[4 * (int64_t)x];
+        int32_t p = uf_ld(u + 4 * (int64_t)x);
         if (p == x) return x;
-        int32_t g = u[4 * (int64_t)p];
+        int32_t g = uf_ld(u + 4 * (int64_t)p);
         if (g == p) return p;
-        u[4 * (int64_t)x] = g;  // path halving: g is an ancestor of x
+        uf_st(u + 4 * (int64_t)x, g);  // path halving: g is an ancestor of x
         x = g;
     }
 }
@@ -106,13 +116,12 @@ __device__ __forceinline__ void flag_or(int *flag, int bits) {
 // root of x in an "upward" forest (every pointer goes to a larger id, roots point to self),
 // compressing as it climbs
 __device__ __forceinline__ int32_t up_find(int32_t *up, int32_t x) {
-    volatile int32_t *u = up;
     while (true) {
-        int32_t p = u[x];
+        int32_t p = uf_ld(up + x);
         if (p == x) return x;
-        int32_t g = u[p];
+        int32_t g = uf_ld(up + p);
         if (g == p) return p;
-        u[x] = g;
+        uf_st(up + x, g);
         x = g;
     }
 }
@@ -432,7 +441,7 @@ __global__ void dc_link(DC c, int b, int j, int64_t nl) {
             if (c.stamp[x] == 2 * j) {  // x lies in an L component of this block
                 const int32_t R = c.lr[uf_find(c.lr, x)].rootedge;
                 // lighter U edges run in earlier lanes: most see their bound already beaten
-                if (((volatile int32_t *)c.parent)[R] > (int32_t)u) atomicMin(&c.parent[R], (int32_t)u);
+                if (uf_ld(c.parent + R) > (int32_t)u) atomicMin(&c.parent[R], (int32_t)u);
                 c.lab[2 * u + s] = (int32_t)(c.n + R);
             }
         }
@@ -458,7 +467,7 @@ __global__ __launch_bounds__(TB) void dc_link_multi(DC c, int b, int j, int64_t 
         for (int k = t; k < SLOTS; k += TB) {
             const int32_t R = skey[k];
             if (R < 0) continue;
-            if (((volatile int32_t *)c.parent)[R] > smin[k]) atomicMin(&c.parent[R], smin[k]);
+            if (uf_ld(c.parent + R) > smin[k]) atomicMin(&c.parent[R], smin[k]);
         }
     };
     const int64_t per = (int64_t)TB * EPT;
@@ -630,7 +639,7 @@ __global__ __launch_bounds__(TB) void dc_mid(DC c, int J, int LM, int LB, int *_
                 for (int k = t; k < KS; k += TB) {
                     const int32_t R = skey[k];
                     if (R < 0) continue;
-                    if (((volatile int32_t *)c.parent)[R] > smin[k]) atomicMin(&c.parent[R], smin[k]);
+                    if (uf_ld(c.parent + R) > smin[k]) atomicMin(&c.parent[R], smin[k]);
                 }
             };
             clear();
