@@ -1329,6 +1329,8 @@ __global__ __launch_bounds__(64) void fo_multi_pre(FoscArr a, int d, const int *
     }
 }
 
+__device__ __forceinline__ bool fo_nonneg(double x) { return x >= 0.0 && !signbit(x); }
+
 // one node of the chain: the host's additions and comparison, in its order
 __device__ __forceinline__ double fo_node(const FoscArr &a, int32_t c, int32_t lt, double st, double lv, double acc,
                                           int32_t &self) {
@@ -1375,6 +1377,9 @@ __global__ __launch_bounds__(64) void fo_walk(FoscArr a, int d, const int *__res
                 s_lv[lane] = lt >= 0 ? a.cp[lt] : 0.0;
             }
             const uint64_t multi = __ballot(lane < cnt && lt == -1);
+            // every staged value >= +0 (no NaN, no -0.0): then st >= prop ? st : prop == max(st, prop)
+            // bit for bit (equal non-negative doubles have equal bits; sums of them stay >= +0)
+            const bool clean = __all(lane >= cnt || (fo_nonneg(s_st[lane]) && fo_nonneg(s_lv[lane])));
             __syncthreads();
             int i = 0;
             if (hi == tlen - 1) {  // the path's bottom: a leaf, its own stability
@@ -1386,6 +1391,21 @@ __global__ __launch_bounds__(64) void fo_walk(FoscArr a, int d, const int *__res
                 const uint64_t mr = i < 64 ? multi & (~0ull << i) : 0;
                 const int e = mr ? min(cnt, __ffsll((unsigned long long)mr) - 1) : cnt;
                 int q = i;
+                if (clean && fo_nonneg(acc)) {  // two dependent ops per node (add, max) instead of four
+                    for (; q + 8 <= e; q += 8) {
+                        double st8[8], lv8[8];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) {
+                            st8[u] = s_st[q + u];
+                            lv8[u] = s_lv[q + u];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; u++) {
+                            acc = fmax(st8[u], acc + lv8[u]);
+                            s_out[q + u] = acc;
+                        }
+                    }
+                }
                 for (; q + 8 <= e; q += 8) {  // binary nodes: uniform LDS reads ahead of the chain
                     double st8[8], lv8[8];
 #pragma unroll
