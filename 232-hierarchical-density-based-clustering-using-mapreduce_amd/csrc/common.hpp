@@ -82,6 +82,7 @@ struct hdb_ctx {
     int boruvka_wave_pts = 64;     // points per scan wave (16/32/64), compacted per 512-position group
     int boruvka_early_pts = 0;     // points per scan wave in rounds < boruvka_early_rounds (0: as above)
     int boruvka_early_rounds = 5;
+    bool boruvka_adj_seed = true;    // K2b: Morton-adjacent pairs across components bound comp_w before the scan
     int trav_pop_test = 0;         // bit 0: Boruvka re-tests a popped node, bit 1: K1t a popped leaf
     bool prim_coop = true;         // cooperative single-launch Prim for 4096 < n <= 65536
     bool prim_coop_plain = true;   // launch it as a plain kernel first (cooperative launches serialise)

@@ -257,6 +257,7 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         if (const char *e = getenv("HDB_FLAT_DEEP_ROOT")) c->flat_deep_root = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_FLAT_DEEP_LINK")) c->flat_deep_link = atoi(e);      // A/B knob
         if (const char *e = getenv("HDB_BOR_EARLY_PTS")) c->boruvka_early_pts = atoi(e);    // A/B knob
+        if (const char *e = getenv("HDB_BOR_ADJ")) c->boruvka_adj_seed = atoi(e) != 0;      // A/B knob
         if (const char *e = getenv("HDB_BOR_EARLY_ROUNDS")) c->boruvka_early_rounds = atoi(e);  // A/B knob
         *out = c;
         return HDB_OK;
@@ -429,6 +430,10 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
     }
     if (k == "trav_pop_test") {
         ctx->trav_pop_test = (int)value;
+        return HDB_OK;
+    }
+    if (k == "boruvka_adj_seed") {
+        ctx->boruvka_adj_seed = value != 0;
         return HDB_OK;
     }
     if (k == "boruvka_wave_pts") {

@@ -1133,6 +1133,34 @@ __global__ __launch_bounds__(WGRP) void group_compact_kernel(const Rec<D> *__res
     }
 }
 
+// Adjacency seeds (round 6).  From round 1 on, a component's bound comes only from last round's
+// edges whose partner is still outside it -- after a merge, mostly none, so comp_w stays "no
+// bound" (NaN bits), no lane is filtered and every wave walks unbounded until some wave
+// publishes.  Any edge between two components is a valid candidate: consecutive sorted
+// positions i, i + 1 in different components (Morton neighbours, so usually close) give one
+// for both, with the scan's exact weight (HDBSCANStar.java:162-168 order).  Only valid edges
+// enter comp_w, so its final value is still the true minimum; every component has such a pair
+// while more than one component remains.
+template <int D>
+__global__ void adj_seed_kernel(const Rec<D> *__restrict__ recs, const int32_t *__restrict__ pcomp, int64_t n,
+                                unsigned long long *__restrict__ comp_w) {
+    HDB_GRID_STRIDE(i, n - 1) {
+        const int32_t ca = pcomp[i], cb = pcomp[i + 1];
+        if (ca == cb) continue;
+        const Rec<D> a = recs[i], b = recs[i + 1];
+        double s = sq_diff(a.x[0], b.x[0]);
+#pragma unroll
+        for (int c = 1; c < D; c++) s = s + sq_diff(a.x[c], b.x[c]);
+        double mrd = sqrt(s);
+        if (a.core > mrd) mrd = a.core;
+        if (b.core > mrd) mrd = b.core;
+        if (!(mrd == mrd)) continue;  // NaN coordinates: no bound
+        const unsigned long long v = dbits(mrd);
+        if (v < __hip_atomic_load(&comp_w[ca], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(&comp_w[ca], v);
+        if (v < __hip_atomic_load(&comp_w[cb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(&comp_w[cb], v);
+    }
+}
+
 // wave descriptors: (start in work) << 8 | count, at the group's exclusive wave offset
 __global__ void wave_desc_kernel(const int32_t *__restrict__ gcnt, const int32_t *__restrict__ woff, int64_t ngroups,
                                  int P, unsigned long long *__restrict__ desc, int32_t *__restrict__ nwaves) {
@@ -2072,6 +2100,8 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             KernelTimer ts(ctx, "boruvka_scan");
             KernelTimer tr(ctx, round_names[round < 8 ? round : 8]);
             const int Pr = round < ctx->boruvka_early_rounds ? PE : P;
+            if (ctx->boruvka_adj_seed && round > 0)
+                hipLaunchKernelGGL(adj_seed_kernel<D>, dim3(g), dim3(256), 0, st, recs, pcomp, n, comp_w);
             hipLaunchKernelGGL(group_compact_kernel<D>, dim3((unsigned)ngroups), dim3(WGRP), 0, st, recs, n,
                                kl ? kl->done : nullptr, bs.lbw, comp_w, Pr, work, gcnt, gwaves);
             size_t tb = 0;
