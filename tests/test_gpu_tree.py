@@ -28,7 +28,7 @@ def eq(a, b):
 def options(ctx, **kw):
     defaults = {"knn_tree": 1, "knn_tree_min_n": 8192, "knn_fp32_screen": 1, "count_evals": 0,
                 "leaf_seed_k": -1, "leaf_list_rounds": 2, "boruvka_seed": 1, "boruvka_wave_pts": 64,
-                "boruvka_early_pts": 0}
+                "boruvka_early_pts": 0, "boruvka_adj_seed": 1}
     try:
         for k, v in kw.items():
             ctx.set_option(k, v)
@@ -195,7 +195,7 @@ def test_exact_mst_device_full_size(star):
 @pytest.mark.parametrize("d", [2, 3, 8])
 def test_exact_mst_seeding_options_equal(ctx, star, d):
     """Every seeding knob (list length, rounds seeded from the lists, previous-round seeds and
-    their carried bounds) changes only which lanes search, never the MST: edge for edge
+    their carried bounds, the Morton-adjacency seeds) changes only which lanes search, never the MST: edge for edge
     equal to the plain constructMSTBoruvka on the same cores (tie-heavy rounded blobs)."""
     X = np.round(blobs(20000, d, 12, 7 * d), 1)
     core, _ = star.exactMST(X, 4, None, 2, selfEdges=False)
@@ -203,6 +203,7 @@ def test_exact_mst_seeding_options_equal(ctx, star, d):
     for kw in ({}, dict(leaf_seed_k=0), dict(leaf_seed_k=7, leaf_list_rounds=64),
                dict(leaf_seed_k=15, leaf_list_rounds=1), dict(leaf_list_rounds=0),
                dict(boruvka_seed=0), dict(boruvka_seed=0, leaf_list_rounds=1),
+               dict(boruvka_adj_seed=0), dict(boruvka_adj_seed=0, boruvka_seed=0, leaf_list_rounds=0),
                # the diagnostic pass at its largest per-wave record count (the
                # record buffer must fit its carve at 16 points per wave)
                dict(count_evals=1, boruvka_wave_pts=16, boruvka_early_pts=16),
