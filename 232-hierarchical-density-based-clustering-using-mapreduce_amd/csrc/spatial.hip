@@ -1554,6 +1554,28 @@ __global__ __launch_bounds__(256) void round_seed_kernel(const Rec<D> *__restric
 }
 
 // ------------------------------------------------------------ K1t: tree kNN
+// XCD-interleaved chunks (round 6, xcb > 0): the dispatcher deals blocks to the 8 XCDs round
+// robin (b and b + 8 share one; placement affects only speed), so block b runs logical block
+// ((q * 8) + b % 8) * xcb + o with (q, o) = divmod(b / 8, xcb): every XCD works through chunks of
+// xcb consecutive blocks (4 * xcb Morton-consecutive tiles), chunks dealt round robin -- a
+// tile's neighbour tiles are mostly fetched by the same XCD (its L2) while dense and sparse
+// regions still spread over all XCDs (round 5's eight contiguous ranges did not).  The grid is a
+// multiple of 8 * xcb (the map is then a bijection); blocks past the tiles exit.
+__device__ __forceinline__ int64_t k1t_block(int xcb) {
+    const int64_t b = blockIdx.x;
+    if (xcb <= 0) return b;
+    const int64_t j = b >> 3, q = j / xcb, o = j - q * xcb;
+    return ((q << 3) + (b & 7)) * xcb + o;
+}
+// chunk size for m chunks per XCD (m <= 0: off): the last chunk holds the remainder, so no XCD
+// gets more than one chunk over the mean
+inline int k1t_xcb(int64_t ntiles, int m) {
+    return m > 0 ? (int)std::max<int64_t>(1, ceil_div(ceil_div(ntiles, 4), 8 * (int64_t)m)) : 0;
+}
+inline unsigned k1t_grid(int64_t ntiles, int xcb) {
+    const int64_t g = ceil_div(ntiles, 4);
+    return (unsigned)(xcb > 0 ? ceil_div(g, 8 * (int64_t)xcb) * 8 * xcb : g);
+}
 // A wave owns query tile t (lane = point).  Its own tile is scanned first (it holds the
 // nearest candidates in Morton order, so the K-th bound is tight from the start), then the
 // BVH is walked nearest-first, skipping any node whose box no lane can still improve on.
@@ -1564,7 +1586,7 @@ template <int D, int K, bool IDX, bool STATS>
 __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kernel(const Rec<D> *__restrict__ recs, int64_t n, int64_t ntiles,
                                                        Bvh bvh, int excl, double *__restrict__ lists,
                                                        int32_t *__restrict__ nb_pos, double *__restrict__ nb_s,
-                                                       int pop_test, unsigned long long *__restrict__ stats) {
+                                                       int pop_test, int xcb, unsigned long long *__restrict__ stats) {
     __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
     __shared__ LRec<D> tile_s[4][BT];
     __shared__ double boxs_s[4][BOXBUF * D];
@@ -1578,7 +1600,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
     const int w = threadIdx.x >> 6;
     int64_t *off_s = lvl_s[w], *cnt_s = lvl_s[w] + MAXLEV + 1;
     // (XCD-contiguous tile ranges were measured again in round 4: 1.56 -> 1.74 ms, not kept)
-    const int64_t t = (int64_t)blockIdx.x * 4 + w;
+    const int64_t t = k1t_block(xcb) * 4 + w;
     if (t >= ntiles) return;
     const int lane = threadIdx.x & 63;
     int32_t *stk = stack_s[w];
@@ -1874,14 +1896,15 @@ static void knn_tree_impl(hdb_ctx *ctx, const double *X, int64_t n, bool excl, d
     if (evals) HIP_CHECK(hipMemsetAsync(evals, 0, 24, ctx->stream));
     {
         KernelTimer t(ctx, "knn_tree");
+        const int xcb = k1t_xcb(sp.ntiles, ctx->k1t_xcd_chunks);
         if (evals)
-            hipLaunchKernelGGL((knn_tree_kernel<D, K, false, true>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256),
+            hipLaunchKernelGGL((knn_tree_kernel<D, K, false, true>), dim3(k1t_grid(sp.ntiles, xcb)), dim3(256),
                                0, ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, excl ? 1 : 0, lists, nullptr, nullptr,
-                               ctx->trav_pop_test, evals);
+                               ctx->trav_pop_test, xcb, evals);
         else
-            hipLaunchKernelGGL((knn_tree_kernel<D, K, false, false>), dim3((unsigned)ceil_div(sp.ntiles, 4)),
+            hipLaunchKernelGGL((knn_tree_kernel<D, K, false, false>), dim3(k1t_grid(sp.ntiles, xcb)),
                                dim3(256), 0, ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, excl ? 1 : 0, lists, nullptr,
-                               nullptr, ctx->trav_pop_test, evals);
+                               nullptr, ctx->trav_pop_test, xcb, evals);
         HIP_CHECK(hipGetLastError());
     }
     if (evals) {
@@ -2299,14 +2322,15 @@ static void exact_leaf_impl(hdb_ctx *ctx, const double *X, int64_t n, int min_pt
     if (stats) HIP_CHECK(hipMemsetAsync(stats, 0, 24, ctx->stream));
     {
         KernelTimer t(ctx, "knn_tree");
+        const int xcb = k1t_xcb(sp.ntiles, ctx->k1t_xcd_chunks);
         if (stats)
-            hipLaunchKernelGGL((knn_tree_kernel<D, K, true, true>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256), 0,
+            hipLaunchKernelGGL((knn_tree_kernel<D, K, true, true>), dim3(k1t_grid(sp.ntiles, xcb)), dim3(256), 0,
                                ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, semantics == HDB_CORE_EXCL_SELF ? 1 : 0,
-                               lists, nb_pos, nb_s, ctx->trav_pop_test, stats);
+                               lists, nb_pos, nb_s, ctx->trav_pop_test, xcb, stats);
         else
-            hipLaunchKernelGGL((knn_tree_kernel<D, K, true, false>), dim3((unsigned)ceil_div(sp.ntiles, 4)), dim3(256),
+            hipLaunchKernelGGL((knn_tree_kernel<D, K, true, false>), dim3(k1t_grid(sp.ntiles, xcb)), dim3(256),
                                0, ctx->stream, sp.recs, n, sp.ntiles, sp.bvh, semantics == HDB_CORE_EXCL_SELF ? 1 : 0,
-                               lists, nb_pos, nb_s, ctx->trav_pop_test, stats);
+                               lists, nb_pos, nb_s, ctx->trav_pop_test, xcb, stats);
         HIP_CHECK(hipGetLastError());
     }
     if (stats) {
