@@ -83,6 +83,7 @@ struct hdb_ctx {
     int boruvka_early_pts = 0;     // points per scan wave in rounds < boruvka_early_rounds (0: as above)
     int boruvka_early_rounds = 5;
     bool boruvka_adj_seed = true;    // K2b: Morton-adjacent pairs across components bound comp_w before the scan
+    int bor_xcd_chunks = 8;        // K2b scan: the same XCD-interleaved chunks over each round's waves
     int k1t_xcd_chunks = 8;        // K1t: Morton chunks per XCD (XCD-interleaved tiles; 0: dispatch order)
     int trav_pop_test = 0;         // bit 0: Boruvka re-tests a popped node, bit 1: K1t a popped leaf
     bool prim_coop = true;         // cooperative single-launch Prim for 4096 < n <= 65536

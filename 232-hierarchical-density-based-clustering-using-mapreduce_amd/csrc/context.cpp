@@ -259,6 +259,7 @@ int hdb_ctx_create(int device, hdb_ctx **out) {
         if (const char *e = getenv("HDB_BOR_EARLY_PTS")) c->boruvka_early_pts = atoi(e);    // A/B knob
         if (const char *e = getenv("HDB_BOR_ADJ")) c->boruvka_adj_seed = atoi(e) != 0;      // A/B knob
         if (const char *e = getenv("HDB_K1T_XCD")) c->k1t_xcd_chunks = atoi(e);             // A/B knob
+        if (const char *e = getenv("HDB_BOR_XCD")) c->bor_xcd_chunks = atoi(e);             // A/B knob
         if (const char *e = getenv("HDB_BOR_EARLY_ROUNDS")) c->boruvka_early_rounds = atoi(e);  // A/B knob
         *out = c;
         return HDB_OK;
@@ -431,6 +432,11 @@ int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value) {
     }
     if (k == "trav_pop_test") {
         ctx->trav_pop_test = (int)value;
+        return HDB_OK;
+    }
+    if (k == "bor_xcd_chunks") {
+        if (value < 0 || value > 4096) return HDB_EINVAL;
+        ctx->bor_xcd_chunks = (int)value;
         return HDB_OK;
     }
     if (k == "k1t_xcd_chunks") {

@@ -87,6 +87,18 @@ __device__ __forceinline__ LRec<D> fetch_rec(const Rec<D> *__restrict__ recs, in
     return r;
 }
 
+// XCD-interleaved chunks (round 6, K1t and the K2b scan; xcb > 0): the dispatcher deals blocks to the 8 XCDs round
+// robin (b and b + 8 share one; placement affects only speed), so block b runs logical block
+// ((q * 8) + b % 8) * xcb + o with (q, o) = divmod(b / 8, xcb): every XCD works through chunks of
+// xcb consecutive blocks (4 * xcb Morton-consecutive tiles), chunks dealt round robin -- a
+// tile's neighbour tiles are mostly fetched by the same XCD (its L2) while dense and sparse
+// regions still spread over all XCDs (round 5's eight contiguous ranges did not).  The grid is a
+// multiple of 8 * xcb (the map is then a bijection); blocks past the tiles exit.
+__device__ __forceinline__ int64_t xcd_chunk_block(int64_t b, int64_t xcb) {
+    if (xcb <= 0) return b;
+    const int64_t j = b >> 3, q = j / xcb, o = j - q * xcb;
+    return ((q << 3) + (b & 7)) * xcb + o;
+}
 // ---------------------------------------------------------------- morton
 // bounding box of X: per-block partial min/max over rows (fmin/fmax ignore NaN), then one
 // block folds the partials
@@ -718,7 +730,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
                                                           int32_t *__restrict__ best_pos,
                                                           const unsigned long long *__restrict__ n_edges_done,
                                                           double *__restrict__ lbw, uint8_t *__restrict__ xact,
-                                                          unsigned long long *__restrict__ stats) {
+                                                          int xm, unsigned long long *__restrict__ stats) {
     __shared__ int32_t stack_s[4][MAXLEV * FAN + 8];
     __shared__ LRec<D> tile_s[4][BT];
     __shared__ double boxs_s[4][BOXBUF * D];
@@ -739,10 +751,18 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
     double *bxs = boxs_s[w];
     int32_t *bxt = boxt_s[w];
     int64_t *off_s = lvl_s[w], *cnt_s = lvl_s[w] + MAXLEV + 1;
-    const int64_t t = (int64_t)blockIdx.x * 4 + w;
     // compacted work list (group_compact_kernel): wave t takes desc[t]'s run of sorted
-    // positions; the grid covers the worst case, waves past the count exit
-    if (t >= *nwaves) return;
+    // positions; the grid covers the worst case (+ 8 xm blocks), waves past the count exit.
+    // xm > 0: xm XCD-interleaved chunks per XCD over this round's blocks (xcd_chunk_block)
+    const int64_t nw = *nwaves;
+    int64_t blk = blockIdx.x;
+    if (xm > 0) {
+        const int64_t xcb = std::max<int64_t>(1, ceil_div(ceil_div(nw, 4), 8 * (int64_t)xm));
+        if (blk >= 8 * xm * xcb) return;
+        blk = xcd_chunk_block(blk, xcb);
+    }
+    const int64_t t = blk * 4 + w;
+    if (t >= nw) return;
     if (*n_edges_done >= (unsigned long long)(n - 1)) return;  // speculative round after the last
     const long long t_start = STATS ? clock64() : 0;
     BorProf<STATS && HDB_BOR_PROF> prof;
@@ -1554,19 +1574,6 @@ __global__ __launch_bounds__(256) void round_seed_kernel(const Rec<D> *__restric
 }
 
 // ------------------------------------------------------------ K1t: tree kNN
-// XCD-interleaved chunks (round 6, xcb > 0): the dispatcher deals blocks to the 8 XCDs round
-// robin (b and b + 8 share one; placement affects only speed), so block b runs logical block
-// ((q * 8) + b % 8) * xcb + o with (q, o) = divmod(b / 8, xcb): every XCD works through chunks of
-// xcb consecutive blocks (4 * xcb Morton-consecutive tiles), chunks dealt round robin -- a
-// tile's neighbour tiles are mostly fetched by the same XCD (its L2) while dense and sparse
-// regions still spread over all XCDs (round 5's eight contiguous ranges did not).  The grid is a
-// multiple of 8 * xcb (the map is then a bijection); blocks past the tiles exit.
-__device__ __forceinline__ int64_t k1t_block(int xcb) {
-    const int64_t b = blockIdx.x;
-    if (xcb <= 0) return b;
-    const int64_t j = b >> 3, q = j / xcb, o = j - q * xcb;
-    return ((q << 3) + (b & 7)) * xcb + o;
-}
 // chunk size for m chunks per XCD (m <= 0: off): the last chunk holds the remainder, so no XCD
 // gets more than one chunk over the mean
 inline int k1t_xcb(int64_t ntiles, int m) {
@@ -1600,7 +1607,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
     const int w = threadIdx.x >> 6;
     int64_t *off_s = lvl_s[w], *cnt_s = lvl_s[w] + MAXLEV + 1;
     // (XCD-contiguous tile ranges were measured again in round 4: 1.56 -> 1.74 ms, not kept)
-    const int64_t t = k1t_block(xcb) * 4 + w;
+    const int64_t t = xcd_chunk_block(blockIdx.x, xcb) * 4 + w;
     if (t >= ntiles) return;
     const int lane = threadIdx.x & 63;
     int32_t *stk = stack_s[w];
@@ -2133,14 +2140,16 @@ static void boruvka_on_index(hdb_ctx *ctx, Spatial<D> &sp, int64_t n, char *extr
             HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, gwaves, woff, (int)ngroups, st));
             hipLaunchKernelGGL(wave_desc_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(ngroups, 256), 4096)),
                                dim3(256), 0, st, gcnt, woff, ngroups, Pr, desc, nwaves);
+            const int xm = ctx->bor_xcd_chunks > 0 ? ctx->bor_xcd_chunks : 0;
+            const unsigned scan_grid = (unsigned)(ceil_div(max_waves, 4) + 8 * xm);
             if (evals)
-                hipLaunchKernelGGL((boruvka_bvh_kernel<D, true>), dim3((unsigned)ceil_div(max_waves, 4)), dim3(256), 0,
+                hipLaunchKernelGGL((boruvka_bvh_kernel<D, true>), dim3(scan_grid), dim3(256), 0,
                                    st, recs, n, ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, work, desc,
-                                   nwaves, ctx->trav_pop_test, inv, best_pos, n_edges, bs.lbw, bs.xact, evals);
+                                   nwaves, ctx->trav_pop_test, inv, best_pos, n_edges, bs.lbw, bs.xact, xm, evals);
             else
-                hipLaunchKernelGGL((boruvka_bvh_kernel<D, false>), dim3((unsigned)ceil_div(max_waves, 4)), dim3(256), 0,
+                hipLaunchKernelGGL((boruvka_bvh_kernel<D, false>), dim3(scan_grid), dim3(256), 0,
                                    st, recs, n, ntiles, bvh, comp_w, best_w, best_s, best_lo, best_hi, work, desc,
-                                   nwaves, ctx->trav_pop_test, inv, best_pos, n_edges, bs.lbw, bs.xact, evals);
+                                   nwaves, ctx->trav_pop_test, inv, best_pos, n_edges, bs.lbw, bs.xact, xm, evals);
         }
         if (evals) {
             std::vector<unsigned long long> recs_h((size_t)BOR_STATS_REC * max_waves);
