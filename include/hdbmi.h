@@ -108,6 +108,12 @@ int hdb_ctx_synchronize(hdb_ctx *ctx);
  *                                  "leaf_list_rounds" (default 2: rounds seeded from the lists);
  *   "boruvka_wave_pts" (default 64; 16/32/64): points per scan wave; "boruvka_early_pts" /
  *                                  "boruvka_early_rounds": another size for the first rounds;
+ *   "boruvka_adj_seed"(default 1): Morton-adjacent pairs across components bound every
+ *                                  component before a Boruvka scan (valid edges only);
+ *   "k1t_xcd_chunks" / "bor_xcd_chunks" (default 8): K1t and the Boruvka scan deal their
+ *                                  Morton-ordered workgroups to the 8 XCDs as 8 interleaved chunks
+ *                                  per XCD (L2 reuse of neighbour tiles; 0: dispatch order) --
+ *                                  placement only, results unchanged;
  *   "trav_pop_test"   (default 0): bit 0 Boruvka, bit 1 K1t re-test a popped node;
  *   "ssort"           (default 1): the Morton order, the MST edge orders, K6's term order and
  *                                  hdb_sort_edges_desc use the sample sort (unique 128-bit keys:
@@ -116,6 +122,8 @@ int hdb_ctx_synchronize(hdb_ctx *ctx);
  *                                  buckets are merged in global memory);
  *   "flat_relabel"    (default 1): hdb_flat_labels renumbers vertex labels in rank order first
  *                                  (locality of the label records; the labels are unchanged);
+ *   "flat_mid_log"    (default 12): hdb_flat_labels runs the divide-and-conquer depths below
+ *                                  2^flat_mid_log ranks per workgroup (<= 10: all global);
  *   "count_evals"     (default 0): K1t/K2b count the pairs they evaluate (read "last_evals"). */
 int hdb_ctx_set_option(hdb_ctx *ctx, const char *name, int64_t value);
 /* Diagnostic counters: "last_evals" = pair evaluations of the last K1t call (count_evals on). */

@@ -28,7 +28,7 @@ def eq(a, b):
 def options(ctx, **kw):
     defaults = {"knn_tree": 1, "knn_tree_min_n": 8192, "knn_fp32_screen": 1, "count_evals": 0,
                 "leaf_seed_k": -1, "leaf_list_rounds": 2, "boruvka_seed": 1, "boruvka_wave_pts": 64,
-                "boruvka_early_pts": 0, "boruvka_adj_seed": 1}
+                "boruvka_early_pts": 0, "boruvka_adj_seed": 1, "k1t_xcd_chunks": 8, "bor_xcd_chunks": 8}
     try:
         for k, v in kw.items():
             ctx.set_option(k, v)
@@ -84,6 +84,18 @@ def test_tree_lists_equal_dense(ctx, star):
         with options(ctx, knn_tree=0):
             b = star.knn(X, k, None, exclSelf=True)
         assert eq(a, b), k
+
+
+@pytest.mark.parametrize("n", [1, 65, 4097, 70000])
+def test_tree_xcd_chunks_lists_equal(ctx, star, n):
+    """K1t's XCD-interleaved chunk map (k1t_xcd_chunks) only places workgroups: the lists are
+    the same with it off, at the default 8 chunks per XCD and at 3 (uneven chunk counts)."""
+    X = blobs(n, 3, 5, 31 + n)
+    out = []
+    for m in (0, 8, 3):
+        with options(ctx, knn_tree=1, knn_tree_min_n=0, k1t_xcd_chunks=m):
+            out.append(star.knn(X, 7, None, exclSelf=True))
+    assert eq(out[0], out[1]) and eq(out[0], out[2])
 
 
 @pytest.mark.parametrize("d", [2, 8, 16])
@@ -204,6 +216,8 @@ def test_exact_mst_seeding_options_equal(ctx, star, d):
                dict(leaf_seed_k=15, leaf_list_rounds=1), dict(leaf_list_rounds=0),
                dict(boruvka_seed=0), dict(boruvka_seed=0, leaf_list_rounds=1),
                dict(boruvka_adj_seed=0), dict(boruvka_adj_seed=0, boruvka_seed=0, leaf_list_rounds=0),
+               # workgroup placement only (XCD-interleaved chunks off, or one chunk per XCD)
+               dict(k1t_xcd_chunks=0, bor_xcd_chunks=0), dict(k1t_xcd_chunks=1, bor_xcd_chunks=1),
                # the diagnostic pass at its largest per-wave record count (the
                # record buffer must fit its carve at 16 points per wave)
                dict(count_evals=1, boruvka_wave_pts=16, boruvka_early_pts=16),
