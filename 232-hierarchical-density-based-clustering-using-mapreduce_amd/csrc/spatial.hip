@@ -516,6 +516,9 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
 #ifndef HDB_K1T_ROWS
 #define HDB_K1T_ROWS 1  // K1t leaf groups needed by few lanes: (query, candidate) pairs in 16-lane rows
 #endif
+#ifndef HDB_K1T_SHFL
+#define HDB_K1T_SHFL 1  // K1t rows: query values by lane shuffles instead of LDS (occupancy; 0: LDS)
+#endif
 #ifndef HDB_K1T_ROWS_MAX
 #define HDB_K1T_ROWS_MAX 16
 #endif
@@ -1601,8 +1604,15 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
     __shared__ int64_t lvl_s[4][2 * (MAXLEV + 1)];
     __shared__ double q_s[4][2 * D];
 #if HDB_K1T_ROWS
+#if HDB_K1T_SHFL
+    // the query lanes' coordinates, bounds and self ids come by lane shuffles (ds_bpermute): 10 KB
+    // less LDS per workgroup, 8 instead of 5 workgroups per CU
+    __shared__ double kq_s[4][BT];
+    __shared__ int32_t kq_lane[4][BT];
+#else
     __shared__ double kq_x[4][BT * D], kq_thr[4][BT], kq_s[4][BT];
     __shared__ int32_t kq_skip[4][BT], kq_lane[4][BT];
+#endif
 #endif
     const int w = threadIdx.x >> 6;
     int64_t *off_s = lvl_s[w], *cnt_s = lvl_s[w] + MAXLEV + 1;
@@ -1637,9 +1647,11 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
     const int32_t skip_self = excl ? mid : -2;
     unsigned long long nev = 0, n_leaf = 0, n_node = 0;
 #if HDB_K1T_ROWS
+#if !HDB_K1T_SHFL
 #pragma unroll
     for (int c = 0; c < D; c++) kq_x[w][lane * D + c] = mx[c];
     kq_skip[w][lane] = skip_self;
+#endif
 #endif
 
     auto needs_vals = [&](const double (&a)[D], const double (&b)[D], int32_t) -> bool {
@@ -1685,10 +1697,15 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
                 const int Kn = __popcll(M);
                 if (Kn <= HDB_K1T_ROWS_MAX) {
                     const int rank = __popcll(M & ((1ull << lane) - 1));
+#if HDB_K1T_SHFL
+                    const double thr0 = buf[K - 1];  // the group-start K-th value of every lane
+                    if (need) kq_lane[w][rank] = lane;
+#else
                     if (need) {
                         kq_thr[w][lane] = buf[K - 1];
                         kq_lane[w][rank] = lane;
                     }
+#endif
                     __builtin_amdgcn_wave_barrier();
                     const int row = lane >> 4, c = lane & 15;
                     const LRec<D> r = cand[q0 + c];
@@ -1696,10 +1713,18 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_K1T_WPE : 1)) void knn_tree_kern
                         const int qr = r0 + row;
                         const bool rowact = qr < Kn;
                         const int ql = kq_lane[w][rowact ? qr : 0];
+#if HDB_K1T_SHFL
+                        double s2 = sq_diff(__shfl(mx[0], ql), r.x[0]);
+#pragma unroll
+                        for (int cc = 1; cc < D; cc++) s2 = s2 + sq_diff(__shfl(mx[cc], ql), r.x[cc]);
+                        const bool pass = rowact & (q0 + c < q1) & (r.id != __shfl(skip_self, ql)) &
+                                          (s2 < __shfl(thr0, ql));
+#else
                         double s2 = sq_diff(kq_x[w][ql * D], r.x[0]);
 #pragma unroll
                         for (int cc = 1; cc < D; cc++) s2 = s2 + sq_diff(kq_x[w][ql * D + cc], r.x[cc]);
                         const bool pass = rowact & (q0 + c < q1) & (r.id != kq_skip[w][ql]) & (s2 < kq_thr[w][ql]);
+#endif
                         if (pass) kq_s[w][lane] = s2;
                         const unsigned long long pm = __ballot(pass);
                         __builtin_amdgcn_wave_barrier();
