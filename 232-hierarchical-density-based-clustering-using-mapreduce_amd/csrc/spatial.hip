@@ -507,6 +507,9 @@ __global__ __launch_bounds__(256) void retag_kernel(Rec<D> *__restrict__ recs, i
 #ifndef HDB_BOR_ROWS
 #define HDB_BOR_ROWS 1  // K2b leaf groups needed by few lanes: (query, candidate) pairs in 16-lane rows
 #endif
+#ifndef HDB_BOR_SHFL
+#define HDB_BOR_SHFL 0  // K2b rows: query values by lane shuffles instead of LDS (occupancy A/B)
+#endif
 #ifndef HDB_BOR_ROWS_MAX
 #define HDB_BOR_ROWS_MAX 8  // ... when at most this many lanes need the group (else the candidate loop; r04 A/B scan: 2.85 ms at 4, 2.81 at 8, 2.84 at 16, 2.97 at 32, 4.1 at 64; K1t at 8: 1.58 vs 1.56 ms at 16)
 #endif
@@ -744,9 +747,15 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
 #if HDB_BOR_ROWS
     // row-batched leaf groups: the wave's query points (staged once) and per group the needing
     // lanes' bounds and the passing pairs' keys
+#if HDB_BOR_SHFL
+    // the query lanes' values come by lane shuffles (ds_bpermute) instead: 12 KB less LDS per
+    // workgroup (6 instead of 4 workgroups per CU)
+    __shared__ int32_t rq_lane[4][BT];
+#else
     __shared__ double rq_x[4][BT * D];
     __shared__ double rq_core[4][BT], rq_sb[4][BT];
     __shared__ int32_t rq_comp[4][BT], rq_id[4][BT], rq_lane[4][BT];
+#endif
     __shared__ double rk_w[4][BT], rk_s[4][BT];
     __shared__ int32_t rk_lo[4][BT], rk_hi[4][BT];
 #endif
@@ -794,7 +803,7 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
 #pragma unroll
         for (int c = 0; c < D; c++) mx[c] = 0;
     }
-#if HDB_BOR_ROWS
+#if HDB_BOR_ROWS && !HDB_BOR_SHFL
 #pragma unroll
     for (int c = 0; c < D; c++) rq_x[w][lane * D + c] = mx[c];
     rq_core[w][lane] = mcore;
@@ -982,10 +991,15 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
             const int K = __popcll(M);
             if (K <= HDB_BOR_ROWS_MAX) {
                 const int rank = __popcll(M & ((1ull << lane) - 1));
+#if HDB_BOR_SHFL
+                const double sb0 = sb;  // the group-start bound of every lane
+                if (need) rq_lane[w][rank] = lane;
+#else
                 if (need) {
                     rq_sb[w][lane] = sb;
                     rq_lane[w][rank] = lane;
                 }
+#endif
                 __builtin_amdgcn_wave_barrier();
                 const int row = lane >> 4, c = lane & 15;
                 const LRec<D> r = cand[q0 + c];  // the row's candidate (4-way LDS broadcast)
@@ -993,18 +1007,28 @@ __global__ __launch_bounds__(256, (D <= 3 ? HDB_BOR_WPE : 1)) void boruvka_bvh_k
                     const int qr = r0 + row;
                     const bool rowact = qr < K;
                     const int ql = rq_lane[w][rowact ? qr : 0];
+#if HDB_BOR_SHFL
+                    // every lane shuffles (the loop is wave-uniform): a shuffle inside the
+                    // divergent branch below would read inactive lanes
+                    double s2 = sq_diff(__shfl(mx[0], ql), r.x[0]);
+#pragma unroll
+                    for (int cc = 1; cc < D; cc++) s2 = s2 + sq_diff(__shfl(mx[cc], ql), r.x[cc]);
+                    const int32_t qcomp = __shfl(mcomp, ql), qid = __shfl(mid, ql);
+                    const double qsb = __shfl(sb0, ql), qc = __shfl(mcore, ql);
+#else
                     double s2 = sq_diff(rq_x[w][ql * D], r.x[0]);
 #pragma unroll
                     for (int cc = 1; cc < D; cc++) s2 = s2 + sq_diff(rq_x[w][ql * D + cc], r.x[cc]);
-                    const bool pair = rowact & (c < nq) & (r.comp != rq_comp[w][ql]);
+                    const int32_t qcomp = rq_comp[w][ql], qid = rq_id[w][ql];
+                    const double qsb = rq_sb[w][ql], qc = rq_core[w][ql];
+#endif
+                    const bool pair = rowact & (c < nq) & (r.comp != qcomp);
                     if (STATS) nev += pair ? 1 : 0;  // pair evaluated for a lane that needs it
-                    const bool pass = pair & (s2 <= rq_sb[w][ql]);  // also drops NaN
+                    const bool pass = pair & (s2 <= qsb);  // also drops NaN
                     if (pass) {
                         double mrd = sqrt(s2);  // HDBSCANStar.java:162-168 order
-                        const double qc = rq_core[w][ql];
                         if (qc > mrd) mrd = qc;
                         if (r.core > mrd) mrd = r.core;
-                        const int32_t qid = rq_id[w][ql];
                         rk_w[w][lane] = mrd;
                         rk_s[w][lane] = s2;
                         rk_lo[w][lane] = qid < r.id ? qid : r.id;
