@@ -1802,10 +1802,17 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     int rounds = 2;
     for (int64_t span = 5; span < m; span *= 5) rounds++;
     rounds = std::min(rounds, 64);
+    // pointer-jumping grids (grid-stride): most launches only see the previous launch's zero
+    // flag and return, so a grid of at most HDB_JUMP_WG workgroups (0: one element per thread;
+    // 256: jump kernels 303 -> 265 us per C2 partition, profiles/r06/jump/)
+#ifndef HDB_JUMP_WG
+#define HDB_JUMP_WG 256
+#endif
+    const unsigned jump_wg = (unsigned)(HDB_JUMP_WG > 0 ? std::min<int64_t>(g / 4 + 1, HDB_JUMP_WG) : g / 4 + 1);
     auto jump_all = [&](int32_t *up) {  // roots of an upward forest, in place
         HIP_CHECK(hipMemsetAsync(jflags, 0, sizeof(int) * 64, st));
         for (int k = 0; k < rounds; k++)
-            hipLaunchKernelGGL(fl_jump, dim3(g / 4 + 1), dim3(1024), 0, st, up, m, k ? jflags + k - 1 : nullptr,
+            hipLaunchKernelGGL(fl_jump, dim3(jump_wg), dim3(1024), 0, st, up, m, k ? jflags + k - 1 : nullptr,
                                jflags + k);
         hipLaunchKernelGGL(fl_jump_check, dim3(1), dim3(64), 0, st, jflags + rounds - 1, err);
     };
@@ -1856,7 +1863,7 @@ void flat_labels_device(hdb_ctx *ctx, const int32_t *va, const int32_t *vb, cons
     jrounds = std::min(jrounds, 64);
     auto jump64 = [&](auto kern, uint64_t *wd, int *flags) {  // flags: jrounds ints, zeroed below
         for (int k = 0; k < jrounds; k++)
-            hipLaunchKernelGGL(kern, dim3(g / 4 + 1), dim3(1024), 0, st, wd, Kp, k ? flags + k - 1 : nullptr, flags + k, err);
+            hipLaunchKernelGGL(kern, dim3(jump_wg), dim3(1024), 0, st, wd, Kp, k ? flags + k - 1 : nullptr, flags + k, err);
         hipLaunchKernelGGL(fl_jump_check, dim3(1), dim3(64), 0, st, flags + jrounds - 1, err);
     };
     // zero: nch, kcur, plen, maxld, hkey (contiguous) and the jump flags
