@@ -10,6 +10,7 @@
 // Host C++ built with -ffp-contract=off so the few host distance evaluations match Java.
 #include <cstdio>
 #include <algorithm>
+#include <deque>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -188,6 +189,7 @@ struct Cl {
     bool hasChildren = false;
     std::vector<int32_t> members;  // TreeSet order (BFS path)
     int32_t node = -1;             // fast path: members = leaves of this dendrogram node
+    int32_t any_member = -1;       // fast path, while a candidate: one member (locates its group)
 };
 
 // Component dendrogram of the (quicksorted) MST edge list, built bottom-up: the component a
@@ -242,16 +244,21 @@ static uint32_t jhash(int32_t k) {
 // instead).  At >= 64 buckets such a bin becomes a tree bin, whose iteration order is not
 // emulated: -1 (HDB_EUNSUPPORTED).  Resizes split buckets order-preservingly, so the keySet
 // order is (bucket at the final capacity, insertion order).
+template <class T>
+static int32_t jlabel(const T &x) { return x.label; }
+template <class T>
+static int32_t jlabel(T *const &x) { return x->label; }
 template <class Label>
 static int64_t jmap_capacity(const std::vector<Label> &aff) {
     int64_t cap = 16;
-    std::vector<int32_t> cnt(cap, 0);
+    thread_local std::vector<int32_t> cnt;  // reused across calls (one call per weight run)
+    cnt.assign(cap, 0);
     auto recount = [&](size_t upto) {
         cnt.assign(cap, 0);
-        for (size_t j = 0; j <= upto; j++) cnt[jhash(aff[j].label) & (uint32_t)(cap - 1)]++;
+        for (size_t j = 0; j <= upto; j++) cnt[jhash(jlabel(aff[j])) & (uint32_t)(cap - 1)]++;
     };
     for (size_t i = 0; i < aff.size(); i++) {
-        const int32_t before = cnt[jhash(aff[i].label) & (uint32_t)(cap - 1)]++;
+        const int32_t before = cnt[jhash(jlabel(aff[i])) & (uint32_t)(cap - 1)]++;
         if (before >= 8) {
             if (cap >= 64) return -1;
             cap *= 2;
@@ -335,6 +342,7 @@ static int construct_cluster_tree_fast(int64_t b, const int32_t *ea, const int32
         clusters.push_back(root);
     }
     std::vector<int32_t> idx_of(2, -1);
+    idx_of.reserve((size_t)b + 2);
     idx_of[1] = 0;
     std::vector<int32_t> pre((size_t)b, -1);  // pre-run node of an endpoint (this run)
     std::vector<int32_t> stk;
@@ -348,9 +356,15 @@ static int construct_cluster_tree_fast(int64_t b, const int32_t *ea, const int32
     };
     std::vector<Piece> pieces;
     std::vector<int32_t> best_of_group;  // scratch: group -> index of its largest piece
+    // per-run scratch kept across runs (one run per distinct weight: ~b runs, so per-run
+    // vectors cost several heap allocations each); entries [0, naff) are live
+    std::deque<Aff> aff_pool;  // a deque: growing it keeps the pointers in `aff` valid
+    std::vector<Aff *> aff;
+    std::vector<Cl> newc;
     int64_t cur = ne - 1;
     while (cur >= 0) {
-        std::vector<Aff> aff;
+        aff.clear();
+        size_t naff = 0;
         const double cw = ew[cur];
         const int64_t run_hi = cur;
         while (cur >= 0 && ew[cur] == cw) {
@@ -363,10 +377,17 @@ static int construct_cluster_tree_fast(int64_t b, const int32_t *ea, const int32
             }
             size_t k = 0;
             for (; k < aff.size(); k++)
-                if (aff[k].label == lab(f)) break;
-            if (k == aff.size()) aff.push_back(Aff{lab(f), (int64_t)aff.size(), {}});
+                if (aff[k]->label == lab(f)) break;
+            if (k == aff.size()) {
+                if (naff == aff_pool.size()) aff_pool.emplace_back();
+                Aff &A = aff_pool[naff++];
+                A.label = lab(f);
+                A.order = (int64_t)aff.size();
+                A.verts.clear();
+                aff.push_back(&A);
+            }
             for (int32_t v : {f, s}) {
-                auto &vs = aff[k].verts;
+                auto &vs = aff[k]->verts;
                 auto it = std::lower_bound(vs.begin(), vs.end(), v);
                 if (it == vs.end() || *it != v) vs.insert(it, v);
             }
@@ -384,9 +405,10 @@ static int construct_cluster_tree_fast(int64_t b, const int32_t *ea, const int32
             }
         }
         if (!pieces.empty()) {
-            std::sort(pieces.begin(), pieces.end(), [](const Piece &x, const Piece &y) {
-                return x.g < y.g || (x.g == y.g && x.node < y.node);
-            });
+            if (pieces.size() > 1)
+                std::sort(pieces.begin(), pieces.end(), [](const Piece &x, const Piece &y) {
+                    return x.g < y.g || (x.g == y.g && x.node < y.node);
+                });
             pieces.erase(std::unique(pieces.begin(), pieces.end(),
                                      [](const Piece &x, const Piece &y) { return x.g == y.g && x.node == y.node; }),
                          pieces.end());
@@ -411,14 +433,22 @@ static int construct_cluster_tree_fast(int64_t b, const int32_t *ea, const int32
         if (aff.empty()) continue;
         const int64_t cap = jmap_capacity(aff);
         if (cap < 0) return HDB_EUNSUPPORTED;
-        std::stable_sort(aff.begin(), aff.end(), [&](const Aff &x, const Aff &y) {
-            uint32_t bx = jhash(x.label) & (uint32_t)(cap - 1), by = jhash(y.label) & (uint32_t)(cap - 1);
-            if (bx != by) return bx < by;
-            return x.order < y.order;
-        });
-        for (auto &A : aff) {
+        // keySet order: (bucket, insertion order) -- a stable insertion sort (a run touches few
+        // labels; std::stable_sort would allocate a buffer per run)
+        for (size_t i = 1; i < aff.size(); i++) {
+            Aff *x = aff[i];
+            const uint32_t bx = jhash(x->label) & (uint32_t)(cap - 1);
+            size_t j = i;
+            while (j > 0 && (jhash(aff[j - 1]->label) & (uint32_t)(cap - 1)) > bx) {
+                aff[j] = aff[j - 1];
+                j--;
+            }
+            aff[j] = x;
+        }
+        for (const Aff *Ap : aff) {
+            const Aff &A = *Ap;
             const int32_t parentLabel = A.label;
-            std::vector<Cl> newc;
+            newc.clear();
             for (int32_t rootV : A.verts) {
                 const int32_t nd = pre[rootV];
                 const int64_t countMembers = D.sum_nb[nd];
@@ -429,7 +459,7 @@ static int construct_cluster_tree_fast(int64_t b, const int32_t *ea, const int32
                     c.birth = cw;
                     c.numPoints = (int32_t)countMembers;
                     c.node = nd;
-                    c.members.push_back(rootV);  // any member: locates the piece's group
+                    c.any_member = rootV;  // locates the piece's group
                     newc.push_back(std::move(c));
                 } else {
                     glabel[group[rootV]] = 0;  // the piece is exactly this group
@@ -443,8 +473,8 @@ static int construct_cluster_tree_fast(int64_t b, const int32_t *ea, const int32
             if (newc.size() >= 2) {
                 for (auto &c : newc) {
                     c.label = nextLabel;
-                    glabel[group[c.members[0]]] = nextLabel;
-                    c.members.clear();
+                    glabel[group[c.any_member]] = nextLabel;
+                    c.any_member = -1;
                     nextLabel++;
                     const int32_t pi = c.parent < (int32_t)idx_of.size() ? idx_of[c.parent] : -1;
                     if (pi >= 0 && clusters[pi].death == JMAX) {
@@ -601,43 +631,50 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
     struct Rec {
         double v[5];
     };
-    std::vector<std::vector<Rec>> adjl;
-    std::vector<int32_t> keyOf;
-    auto find_key = [&](int32_t key) -> int {
-        for (size_t i = 0; i < keyOf.size(); i++)
-            if (keyOf[i] == key) return (int)i;
-        return -1;
+    struct Span {  // one label's list in the flat record array
+        Rec *b_, *e_;
+        bool empty() const { return b_ == e_; }
+        Rec &operator[](size_t i) { return b_[i]; }
+        Rec *begin() { return b_; }
+        Rec *end() { return e_; }
     };
     // label -> slot index (labels are small ints; dense lookup table)
     int32_t maxlab = 1;
     for (auto *c : tree) maxlab = std::max(maxlab, c->label);
     std::vector<int> slot(maxlab + 2, -1);
-    auto get = [&](int32_t key) -> std::vector<Rec> * {
-        if (key < 0 || key > maxlab || slot[key] < 0) return nullptr;
-        return &adjl[slot[key]];
-    };
+    int nslots = 0;
     auto put = [&](int32_t key) {
-        if (key >= 0 && key <= maxlab && slot[key] < 0) {
-            slot[key] = (int)adjl.size();
-            adjl.emplace_back();
-            keyOf.push_back(key);
-        }
+        if (key >= 0 && key <= maxlab && slot[key] < 0) slot[key] = nslots++;
     };
-    (void)find_key;
     // for par in tree: for ch in tree: par.label == ch.parent -> adj[par] += ch (tree order);
-    // labels are unique, so one pass over the children builds the same lists
+    // labels are unique, so one pass over the children builds the same lists -- laid out as one
+    // flat array (counted, then filled in tree order: each list keeps the child order)
     std::vector<Cl *> by_label(maxlab + 2, nullptr);
     for (auto *c : tree) by_label[c->label] = c;
+    auto parent_of = [&](const Cl *ch) -> Cl * {
+        if (ch->parent < 0 || ch->parent > maxlab) return nullptr;
+        return by_label[ch->parent];
+    };
     for (auto *par : tree)
         if (!par->hasChildren) put(par->label);
-    for (auto *ch : tree) {
-        if (ch->parent < 0 || ch->parent > maxlab) continue;
-        Cl *par = by_label[ch->parent];
-        if (!par) continue;
-        put(par->label);
-        Rec r{{par->stability, (double)ch->label, ch->stability, 1.0, (double)par->parent}};
-        get(par->label)->push_back(r);
-    }
+    for (auto *ch : tree)
+        if (Cl *par = parent_of(ch)) put(par->label);
+    std::vector<int64_t> roff((size_t)nslots + 1, 0);
+    for (auto *ch : tree)
+        if (Cl *par = parent_of(ch)) roff[(size_t)slot[par->label] + 1]++;
+    for (int i = 0; i < nslots; i++) roff[i + 1] += roff[i];
+    std::vector<Rec> recs((size_t)roff[nslots]);
+    std::vector<int64_t> rpos(roff.begin(), roff.end() - 1);
+    for (auto *ch : tree)
+        if (Cl *par = parent_of(ch))
+            recs[(size_t)rpos[slot[par->label]]++] =
+                Rec{{par->stability, (double)ch->label, ch->stability, 1.0, (double)par->parent}};
+    std::vector<Span> spans((size_t)nslots);
+    for (int i = 0; i < nslots; i++) spans[i] = Span{recs.data() + roff[i], recs.data() + roff[i + 1]};
+    auto get = [&](int32_t key) -> Span * {
+        if (key < 0 || key > maxlab || slot[key] < 0) return nullptr;
+        return &spans[slot[key]];
+    };
     // Collections.sort by birth level (stable)
     using fclk = std::chrono::steady_clock;
     auto fus = [](fclk::time_point a, fclk::time_point b) {
