@@ -158,11 +158,15 @@ int quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne) {
         const double pv = wt(s);  // selectPivotIndex always returns startIndex (:158)
         swp(s, e);
         int64_t low = s;
-        for (int64_t i = s; i < e; i++)
-            if (wt(i) < pv) {
-                swp(i, low);
-                low++;
-            }
+        E *R = r.data();
+        for (int64_t i = s; i < e; i++) {  // if (w[i] < pv) swap(i, low++), without the branch
+            const E x = R[i];
+            const bool c = x.w < pv;
+            const int64_t dst = c ? low : i;  // not taken: R[i] rewritten with itself
+            R[i] = R[dst];
+            R[dst] = x;
+            low += c;
+        }
         swp(low, e);
         const int64_t pivot = low;
         if (pivot > s + 1) {

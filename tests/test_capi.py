@@ -58,6 +58,27 @@ def test_quicksort_random_vs_oracle(pkg, oracle):
         assert np.array_equal(ug.getVerticeA(), oa) and np.array_equal(ug.getEges(), ow)
 
 
+def test_quicksort_ties_nan_large_vs_oracle(pkg, oracle):
+    """The branch-free partition (round 6) keeps the reference's swaps: heavy ties, NaN weights
+    (never '<' the pivot), already-sorted and reversed runs, bit-equal to the oracle."""
+    rng = np.random.default_rng(11)
+    for n, kind in ((4000, "ties"), (3001, "nan"), (2048, "sorted"), (2049, "reversed")):
+        w = np.round(rng.uniform(0, 2, n), 1)
+        if kind == "nan":
+            w[rng.integers(0, n, 40)] = np.nan
+        elif kind == "sorted":
+            w = np.sort(w)
+        elif kind == "reversed":
+            w = np.sort(w)[::-1].copy()
+        a = rng.integers(0, 500, n).astype(np.int32)
+        b = rng.integers(0, 500, n).astype(np.int32)
+        ug = pkg.UndirectedGraph(a.copy(), b.copy(), w.copy())
+        ug.quicksortByEdgeWeight()
+        oa, ob, ow = oracle.quicksort_edges(a, b, w)
+        assert np.array_equal(ug.getVerticeA(), oa) and np.array_equal(ug.getVericeB(), ob), kind
+        assert np.array_equal(ug.getEges().view(np.uint64), np.asarray(ow).view(np.uint64)), kind
+
+
 def test_distance_names(pkg):
     assert pkg.EuclideanDistance().getName() == "euclidean"
     assert pkg.CosineSimilarity().getName() == "cosine"
