@@ -685,8 +685,14 @@ static int find_prominent(std::vector<Cl> &cl, const double *rep, const double *
         return (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
     };
     const auto f0 = fclk::now();
-    std::vector<Cl *> sorted = tree;
-    std::stable_sort(sorted.begin(), sorted.end(), [](const Cl *a, const Cl *b) { return a->birth < b->birth; });
+    // (birth, position) pairs sorted with the same comparison on a copy of the key: the same
+    // stable order without chasing a Cl pointer per comparison
+    std::vector<std::pair<double, int32_t>> kb(tree.size());
+    for (size_t i = 0; i < tree.size(); i++) kb[i] = {tree[i]->birth, (int32_t)i};
+    std::stable_sort(kb.begin(), kb.end(),
+                     [](const std::pair<double, int32_t> &a, const std::pair<double, int32_t> &b) { return a.first < b.first; });
+    std::vector<Cl *> sorted(tree.size());
+    for (size_t i = 0; i < tree.size(); i++) sorted[i] = tree[kb[i].second];
     for (int64_t o = 0; o < b; o++) flat[o] = 0;
     std::vector<char> sol(maxlab + 2, 0);
     for (auto *c : sorted) sol[c->label] = 1;
