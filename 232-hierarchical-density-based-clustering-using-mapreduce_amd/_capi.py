@@ -105,6 +105,7 @@ def lib():
             "hdb_bubble_core_distances": [vp, dp, ip, dp, dp, i64, i32, i32, i32, dp],
             "hdb_bubble_prim_mst": [vp, dp, dp, dp, ip, dp, i64, i32, i32, i32, ip, ip, dp],
             "hdb_local_model": [vp, dp, dp, i64, i32, i32, i32, i32, ip, ip, ip, dp, ip, ip, dp, lp],
+            "hdb_local_model_cores": [vp, dp, dp, i64, i32, i32, i32, i32, dp, ip, ip, ip, dp, ip, ip, dp, lp],
             "hdb_quicksort_edges": [ip, ip, dp, i64],
             "hdb_sort_edges_desc": [vp, ip, ip, dp, i64],
             "hdb_merge_sorted_runs": [vp, ip, ip, dp, lp, i32, ip, ip, dp],
@@ -139,7 +140,7 @@ EXPORTED = ["hdb_ctx_create", "hdb_ctx_destroy", "hdb_ctx_set_stream", "hdb_ctx_
             "hdb_ctx_get_stat", "hdb_ctx_kernel_time", "hdb_ctx_synchronize", "hdb_last_error", "hdb_version",
             "hdb_distance_rows", "hdb_core_distances", "hdb_knn", "hdb_prim_mst", "hdb_prim_mst_batched",
             "hdb_leaf_msts", "hdb_mst_boruvka", "hdb_exact_mst", "hdb_nearest_sample", "hdb_bubble_stats",
-            "hdb_bubble_partials", "hdb_bubble_combine", "hdb_bubble_core_distances", "hdb_bubble_prim_mst", "hdb_local_model", "hdb_quicksort_edges",
+            "hdb_bubble_partials", "hdb_bubble_combine", "hdb_bubble_core_distances", "hdb_bubble_prim_mst", "hdb_local_model", "hdb_local_model_cores", "hdb_quicksort_edges",
             "hdb_merge_sorted_runs", "hdb_sort_edges_desc", "hdb_flat_labels", "hdb_format_double", "hdb_parse_points",
             "hdb_format_mst_records", "hdb_parse_mst_records", "hdb_comm_unique_id", "hdb_comm_init",
             "hdb_comm_destroy", "hdb_free", "hdb_copy", "hdb_merge_edges", "hdb_local_mst_ids"]

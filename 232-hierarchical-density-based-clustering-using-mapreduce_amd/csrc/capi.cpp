@@ -380,9 +380,12 @@ int hdb_quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne) {
     return rc;
 }
 
-int hdb_local_model(hdb_ctx *ctx, const double *rep, const double *info, int64_t b, int32_t d, int32_t min_pts,
-                    int32_t min_cl_size, int32_t metric, int32_t *labels, int32_t *mst_va, int32_t *mst_vb,
-                    double *mst_w, int32_t *ic_va, int32_t *ic_vb, double *ic_w, int64_t *n_ic) {
+// core_in (nullable, host, b values): the bubble core distances already computed by
+// hdb_bubble_core_distances on the same (rep, nB, eB, nnB) -- the model then starts at the Prim
+static int local_model_impl(hdb_ctx *ctx, const double *rep, const double *info, int64_t b, int32_t d,
+                            int32_t min_pts, int32_t min_cl_size, int32_t metric, const double *core_in,
+                            int32_t *labels, int32_t *mst_va, int32_t *mst_vb, double *mst_w, int32_t *ic_va,
+                            int32_t *ic_vb, double *ic_w, int64_t *n_ic) {
     return guarded(ctx, [&] {
         check_metric(metric);
         if (b < 1 || d <= 0 || !rep || !info || !labels || min_pts < 1) HDB_THROW(HDB_EINVAL, "bad arguments");
@@ -403,7 +406,10 @@ int hdb_local_model(hdb_ctx *ctx, const double *rep, const double *info, int64_t
         };
         auto t0 = clk::now();
         std::vector<double> core;
-        bubble_core_impl(ctx, rep_h.data(), nB.data(), eB.data(), nnB.data(), b, d, min_pts, metric, core);
+        if (core_in)
+            core.assign(core_in, core_in + b);
+        else
+            bubble_core_impl(ctx, rep_h.data(), nB.data(), eB.data(), nnB.data(), b, d, min_pts, metric, core);
         auto t1 = clk::now();
         const int64_t ne = 2 * b - 1;
         std::vector<int32_t> mva(ne), mvb(ne);
@@ -441,6 +447,25 @@ int hdb_local_model(hdb_ctx *ctx, const double *rep, const double *info, int64_t
         if (ic_w) std::copy(iw.begin(), iw.begin() + nic, ic_w);
         if (n_ic) *n_ic = nic;
     });
+}
+
+int hdb_local_model(hdb_ctx *ctx, const double *rep, const double *info, int64_t b, int32_t d, int32_t min_pts,
+                    int32_t min_cl_size, int32_t metric, int32_t *labels, int32_t *mst_va, int32_t *mst_vb,
+                    double *mst_w, int32_t *ic_va, int32_t *ic_vb, double *ic_w, int64_t *n_ic) {
+    return local_model_impl(ctx, rep, info, b, d, min_pts, min_cl_size, metric, nullptr, labels, mst_va, mst_vb,
+                            mst_w, ic_va, ic_vb, ic_w, n_ic);
+}
+
+int hdb_local_model_cores(hdb_ctx *ctx, const double *rep, const double *info, int64_t b, int32_t d,
+                          int32_t min_pts, int32_t min_cl_size, int32_t metric, const double *core, int32_t *labels,
+                          int32_t *mst_va, int32_t *mst_vb, double *mst_w, int32_t *ic_va, int32_t *ic_vb,
+                          double *ic_w, int64_t *n_ic) {
+    if (!core) {
+        set_error("hdb_local_model_cores: core is required");
+        return HDB_EINVAL;
+    }
+    return local_model_impl(ctx, rep, info, b, d, min_pts, min_cl_size, metric, core, labels, mst_va, mst_vb, mst_w,
+                            ic_va, ic_vb, ic_w, n_ic);
 }
 
 int hdb_sort_edges_desc(hdb_ctx *ctx, int32_t *va, int32_t *vb, double *w, int64_t ne) {

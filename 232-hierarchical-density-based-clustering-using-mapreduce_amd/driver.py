@@ -73,7 +73,7 @@ class MRHDBSCANStar:
                  seed=20210101, distanceFunction=None, all_inter_edges=True, max_levels=64, ctx=None,
                  device=0, flat_labels=True, profile=False, exact_prim_leaves=False, group=None,
                  prim_leaf_max=LEAF_PRIM_MAX, model_threads=4, defer_leaves=True, bubble_slices=BUBBLE_SLICES,
-                 emulate_ranks=()):
+                 emulate_ranks=(), cores_first=False):
         self.minPts = minPts
         self.minClSize = minClSize
         self.processing_units = processing_units
@@ -98,6 +98,11 @@ class MRHDBSCANStar:
         # a level's local models run concurrently, one host thread (own context and stream)
         # each: a bubble Prim occupies only ceil(b / 1024) CUs
         self.model_threads = int(os.environ.get("HDB_MODEL_THREADS", model_threads))
+        # cores_first: a rank holding several models of a level computes all their bubble core
+        # distances before any of their Prims (hdb_local_model_cores; same cores, same outputs).
+        # Measured on C5 (round 6): no change (emulated N = 8 local models 1.956 vs 1.951 s), so
+        # off by default
+        self.cores_first = bool(int(os.environ.get("HDB_CORES_FIRST", int(cores_first))))
         # leaves are end points of the subset tree: nothing later in the loop reads their edges,
         # so they can wait until the level loop is done and then run as ONE batch over the
         # whole job (global LPT over the ranks, one batched Prim launch for every small leaf)
@@ -364,22 +369,36 @@ class MRHDBSCANStar:
             # local models: LPT over the ranks on b^2, results gathered, applied in subset order
             nonempty_of = [np.nonzero(info_h[s_off[i]:s_off[i + 1], 2] > 0)[0] for i in range(len(big))]  # D4
             owner = P.lpt([int(ne.shape[0]) ** 2 for ne in nonempty_of], world)
-            def model(i):
+            core_s = {}  # cores-first: seconds of each model's core pass (added to its task time)
+
+            def model(i, core=None):
                 import time
                 t0 = time.perf_counter()
                 try:
-                    return model_body(i)
+                    return model_body(i, core)
                 finally:
-                    self._task("local_models", float(nonempty_of[i].shape[0]) ** 2, time.perf_counter() - t0)
+                    self._task("local_models", float(nonempty_of[i].shape[0]) ** 2,
+                               time.perf_counter() - t0 + core_s.get(i, 0.0))
 
-            def model_body(i):
+            def model_core(i):
+                import time
+                t0 = time.perf_counter()
+                a, b = s_off[i], s_off[i + 1]
+                nonempty = nonempty_of[i]
+                core = None
+                if nonempty.shape[0] >= 2:
+                    core = self._model_cores(rep_h[a:b][nonempty], info_h[a:b][nonempty])
+                core_s[i] = time.perf_counter() - t0
+                return core
+
+            def model_body(i, core=None):
                 a, b = s_off[i], s_off[i + 1]
                 nonempty = nonempty_of[i]
                 if nonempty.shape[0] < 2:
                     return None, None, None
                 try:
                     labels, (iva, ivb, iw) = self._local_model(rep_h[a:b][nonempty], info_h[a:b][nonempty],
-                                                               threaded=True)
+                                                               threaded=True, core=core)
                 except A.HdbError as e:  # D10: the reference's own exceptions only
                     if e.code > -10:
                         raise
@@ -390,17 +409,18 @@ class MRHDBSCANStar:
                     inter = (gid[iva], gid[ivb], iw) if self.all_inter_edges else (iva[:1], ivb[:1], iw[:1])
                 return labels, None, inter
 
+            def run_models(grp, fn):
+                """one rank's models as the pool runs them (cores-first when it holds several)"""
+                if self.cores_first and len(grp) > 1 and self.model_threads > 1:
+                    cores = dict(zip(grp, self._run_group(model_core, grp)))
+                    return dict(zip(grp, self._run_group(lambda i: fn(i, cores[i]), grp)))
+                return dict(zip(grp, self._run_group(fn, grp)))
+
             mine = [i for i in range(len(big)) if owner[i] == rank]
-            if len(mine) > 1 and self.model_threads > 1:
-                if self._pool is None:
-                    from concurrent.futures import ThreadPoolExecutor
-                    self._pool = ThreadPoolExecutor(self.model_threads)
-                results = dict(zip(mine, self._pool.map(model, mine)))
-            else:
-                results = {i: model(i) for i in mine}
+            results = run_models(mine, model)
             if self.profile and self.emulate_ranks and world == 1:
                 self._lvl["emulated_local_models"] = self._emulate(
-                    [int(ne.shape[0]) ** 2 for ne in nonempty_of], lambda grp: self._run_group(model_body, grp))
+                    [int(ne.shape[0]) ** 2 for ne in nonempty_of], lambda grp: run_models(grp, model_body))
             if world > 1:
                 for part in P.allgather_object(results, self.group):
                     results.update(part)
@@ -567,9 +587,24 @@ class MRHDBSCANStar:
         A.check(A.lib().hdb_bubble_combine(c.h, pls.data_ptr(), pss.data_ptr(), pn.data_ptr(), Sl, nb, d, ls.data_ptr(),
                                            ss.data_ptr(), rep.data_ptr(), info.data_ptr()), "CombineStep merge")
 
-    def _local_model(self, rep, info, threaded=False):
+    def _model_cores(self, rep, info):
+        """HdbscanDataBubbles.calculateCoreDistancesBubbles for one model (this thread's context):
+        the cores hdb_local_model computes first, from the same (rep, nB, eB, nnB)"""
+        rep = np.ascontiguousarray(rep, np.float64)
+        info = np.ascontiguousarray(info, np.float64)
+        b, d = rep.shape
+        eB, nnB = np.ascontiguousarray(info[:, 0]), np.ascontiguousarray(info[:, 1])
+        nB = np.ascontiguousarray(info[:, 2].astype(np.int32))  # (int) info[i * 3 + 2], as hdb_local_model
+        core = np.zeros(b)
+        c = A.Context.get(self.device)
+        A.check(A.lib().hdb_bubble_core_distances(c.h, A.ptr(rep), A.ptr(nB), A.ptr(eB), A.ptr(nnB), b, d, self.minPts,
+                                                  self.metric, A.ptr(core)), "calculateCoreDistancesBubbles")
+        return core
+
+    def _local_model(self, rep, info, threaded=False, core=None):
         """LocalModelReduceByKey.java:88-104 body (D4 ids) -> (labels, inter-cluster edges).
-        threaded: this thread's own context (private stream) instead of the driver's."""
+        threaded: this thread's own context (private stream) instead of the driver's; core: the
+        model's bubble cores computed beforehand (_model_cores)."""
         rep = np.ascontiguousarray(rep, np.float64)
         info = np.ascontiguousarray(info, np.float64)
         b, d = rep.shape
@@ -579,8 +614,15 @@ class MRHDBSCANStar:
         iva, ivb, iw = np.zeros(ne, np.int32), np.zeros(ne, np.int32), np.zeros(ne)
         nic = np.zeros(1, np.int64)
         c = A.Context.get(self.device) if threaded else self._c()
-        A.check(A.lib().hdb_local_model(c.h, A.ptr(rep), A.ptr(info), b, d, self.minPts, self.minClSize, self.metric,
-                                        A.ptr(labels), A.ptr(mva), A.ptr(mvb), A.ptr(mw), A.ptr(iva), A.ptr(ivb),
-                                        A.ptr(iw), A.ptr(nic)), "LocalModelReduceByKey")
+        if core is not None:
+            core = np.ascontiguousarray(core, np.float64)
+            A.check(A.lib().hdb_local_model_cores(c.h, A.ptr(rep), A.ptr(info), b, d, self.minPts, self.minClSize,
+                                                  self.metric, A.ptr(core), A.ptr(labels), A.ptr(mva), A.ptr(mvb),
+                                                  A.ptr(mw), A.ptr(iva), A.ptr(ivb), A.ptr(iw), A.ptr(nic)),
+                    "LocalModelReduceByKey")
+        else:
+            A.check(A.lib().hdb_local_model(c.h, A.ptr(rep), A.ptr(info), b, d, self.minPts, self.minClSize,
+                                            self.metric, A.ptr(labels), A.ptr(mva), A.ptr(mvb), A.ptr(mw), A.ptr(iva),
+                                            A.ptr(ivb), A.ptr(iw), A.ptr(nic)), "LocalModelReduceByKey")
         k = int(nic[0])
         return labels, (iva[:k], ivb[:k], iw[:k])

@@ -241,6 +241,15 @@ int hdb_local_model(hdb_ctx *ctx, const double *rep, const double *info, int64_t
                     int32_t min_cl_size, int32_t metric, int32_t *labels, int32_t *mst_va, int32_t *mst_vb,
                     double *mst_w, int32_t *ic_va, int32_t *ic_vb, double *ic_w, int64_t *n_ic);
 
+/* hdb_local_model from precomputed bubble core distances (host, b values: hdb_bubble_core_distances
+ * of the same rep / nB = (int) info[:, 2] / eB = info[:, 0] / nnB = info[:, 1], min_pts, metric) --
+ * the same outputs; lets a caller compute every model's cores of a level before any model's Prim
+ * (round 6: a Prim holds its CUs for its whole run and slows concurrent work). */
+int hdb_local_model_cores(hdb_ctx *ctx, const double *rep, const double *info, int64_t b, int32_t d, int32_t min_pts,
+                          int32_t min_cl_size, int32_t metric, const double *core, int32_t *labels, int32_t *mst_va,
+                          int32_t *mst_vb, double *mst_w, int32_t *ic_va, int32_t *ic_vb, double *ic_w,
+                          int64_t *n_ic);
+
 /* UndirectedGraph.quicksortByEdgeWeight (UndirectedGraph.java:93-124), in place, host. */
 int hdb_quicksort_edges(int32_t *va, int32_t *vb, double *w, int64_t ne);
 
